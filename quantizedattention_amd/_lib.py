@@ -1,0 +1,94 @@
+"""ctypes binding of libqattn.so — the C-ABI boundary declared in include/qattn.h.
+
+The library is loaded after ``torch`` so that its ``libamdhip64.so.7`` dependency resolves to the
+HIP runtime torch already mapped (one runtime per process; torch streams are valid handles).
+There is no fallback: if the library is missing or a call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "libqattn.so"
+
+_c_long = ctypes.c_long
+_c_int = ctypes.c_int
+_c_float = ctypes.c_float
+_vp = ctypes.c_void_p
+
+# name -> argtypes (restype is always int status: 0 ok, 1 invalid argument, 2 launch failure)
+SIGNATURES = {
+    "qattn_int8_quant": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_int, _c_int, _vp],
+    "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
+    "qattn_int8_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _c_float, _vp],
+    "qattn_int8_bwd_prep": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
+    "qattn_int8_attn_bwd": [_vp] * 16 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
+    "qattn_bf16_fwd": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
+    "qattn_bf16_bwd_prep": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
+    "qattn_bf16_bwd": [_vp] * 12 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
+    "qattn_jvp_fwd": [_vp] * 9 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
+    "qattn_probe_mfma_i8": [_vp, _vp, _vp, _vp],
+    "qattn_probe_mfma_f16": [_vp, _vp, _vp, _vp],
+    "qattn_probe_tr16": [_vp, _vp, _vp],
+    "qattn_probe_int8_attn_dbg": [_vp] * 7 + [_c_long, _c_long, _c_float, _vp, _vp],
+}
+
+_lib = None
+
+
+class QAttnError(RuntimeError):
+    pass
+
+
+def load(path: os.PathLike | None = None) -> ctypes.CDLL:
+    """Load (once) and type the library; raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise QAttnError(
+            f"{p} not found: build it with `python -m quantizedattention_amd.build` "
+            "(there is no CPU fallback)")
+    lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    lib = load()
+    return [n for n in SIGNATURES if hasattr(lib, n)]
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def call(name: str, *args) -> None:
+    fn = getattr(load(), name)
+    rc = fn(*args)
+    if rc == 1:
+        raise QAttnError(f"{name}: unsupported shape/argument (status 1)")
+    if rc != 0:
+        raise QAttnError(f"{name}: kernel launch failed (status {rc})")
+
+
+def require_gpu(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if not t.is_cuda:
+            raise QAttnError("qattn kernels run on the GPU only; got a tensor on "
+                             f"{t.device} (no CPU fallback by design)")

@@ -1,0 +1,141 @@
+"""Drop-in for ``attention_bf16`` of selau642/QuantizedAttention, backed by gfx950 HIP kernels.
+
+Public names (same signatures, outputs and assertion messages):
+  FlashAttention_2_BF16_autograd_function   attention_bf16.py:16-85
+  flash_atten_2_bf16                        attention_bf16.py:87-105
+  helion_atten_bf16_fwd_training            attention_bf16.py:107-296
+  helion_flash_atten_2_algo_4_bwd           attention_bf16.py:299-448
+  baseline_pytorch_attention                attention_bf16.py:450-478
+
+Forward: bf16 FlashAttention with the reference's "multiple-max" beta rule emulated at its pinned
+k-tile of 16 (bf16:736).  Backward: FA2 algorithm 4 with the build-contract fixes of SURVEY F3
+(dS = P*(dP-D), sm_scale, deterministic dQ).
+"""
+from __future__ import annotations
+
+import math
+from typing import Tuple
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+from ._baseline import baseline_pytorch_attention  # noqa: F401
+
+__all__ = [
+    "FlashAttention_2_BF16_autograd_function", "flash_atten_2_bf16",
+    "helion_atten_bf16_fwd_training", "helion_flash_atten_2_algo_4_bwd",
+    "baseline_pytorch_attention",
+]
+
+KT = 16  # k-tile of the beta rule (reference tuned config, bf16:736)
+
+
+def _f32(x: float) -> float:
+    return float(torch.tensor(x, dtype=torch.float32))
+
+
+def _check(q, k, v):
+    batch, head, q_tokens, q_head_dim = q.shape
+    k_batch, k_head, k_tokens, k_head_dim = k.shape
+    v_batch, v_head, v_tokens, v_head_dim = v.shape
+    assert k_tokens == v_tokens, "input k_tokens must match v_tokens"  # bf16:154
+    assert q_head_dim == k.size(-1) == v.size(-1), \
+        "all head dimensions must match for q, k, v tensors"  # bf16:155
+    if not (q.shape[:2] == k.shape[:2] == v.shape[:2]):
+        raise _lib.QAttnError("qattn bf16: batch/head dims of q, k, v must match")
+    if q_tokens % 32 or k_tokens % 32:
+        raise _lib.QAttnError("qattn bf16: token counts must be multiples of 32")
+    if q_head_dim not in (64, 128):
+        raise _lib.QAttnError("qattn bf16: head_dim must be 64 or 128")
+
+
+def helion_atten_bf16_fwd_training(
+    q_fp16_input: torch.Tensor,
+    k_fp16_input: torch.Tensor,
+    v_bf16_input: torch.Tensor,
+    causal: bool,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """bf16:111-296 -> (O fp32 [B,H,S,D], lse fp32 [B*H, S], base-2 units)."""
+    _check(q_fp16_input, k_fp16_input, v_bf16_input)
+    _lib.require_gpu(q_fp16_input, k_fp16_input, v_bf16_input)
+    q = q_fp16_input.to(torch.float16).contiguous()
+    k = k_fp16_input.to(torch.float16).contiguous()
+    v = v_bf16_input.to(torch.bfloat16).contiguous()
+    B, H, S, D = q.shape
+    Sk = k.shape[2]
+    O = torch.empty((B, H, S, D), dtype=torch.float32, device=q.device)
+    lse = torch.empty((B * H, S), dtype=torch.float32, device=q.device)
+    qks = _f32(1.0 / math.sqrt(D) * 1.44269504)
+    _lib.call("qattn_bf16_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(O), _lib.ptr(lse),
+              B * H, S, Sk, D, int(bool(causal)), qks, _lib.stream_of(q))
+    return O, lse
+
+
+def helion_flash_atten_2_algo_4_bwd(
+    q_input: torch.Tensor,
+    k_input: torch.Tensor,
+    v_input: torch.Tensor,
+    O_input: torch.Tensor,
+    lse_input: torch.Tensor,
+    causal: bool,
+    dO_input: torch.Tensor,
+):
+    """bf16:309-448 (corrected) -> fp32 (dq, dk, dv)."""
+    _check(q_input, k_input, v_input)
+    _lib.require_gpu(q_input, k_input, v_input, O_input, lse_input, dO_input)
+    q = q_input.to(torch.float16).contiguous()
+    k = k_input.to(torch.float16).contiguous()
+    v = v_input.to(torch.bfloat16).contiguous()
+    O = O_input.to(torch.float32).contiguous()
+    dO = dO_input.to(torch.float32).contiguous()
+    lse = lse_input.to(torch.float32).contiguous()
+    B, H, S, D = q.shape
+    Sk = k.shape[2]
+    dev = q.device
+    st = _lib.stream_of(q)
+    dO_bf = torch.empty((B, H, S, D), dtype=torch.bfloat16, device=dev)
+    Drow = torch.empty((B * H, S), dtype=torch.float32, device=dev)
+    _lib.call("qattn_bf16_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(dO_bf), _lib.ptr(Drow), None,
+              B * H, S, D, st)
+    dq = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+    dk = torch.empty((B, H, Sk, D), dtype=torch.float32, device=dev)
+    dv = torch.empty((B, H, Sk, D), dtype=torch.float32, device=dev)
+    qks = _f32(1.0 / math.sqrt(D) * 1.44269504)
+    sms = _f32(1.0 / math.sqrt(D))
+    _lib.call("qattn_bf16_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(lse),
+              _lib.ptr(Drow), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), None, None, None,
+              B * H, S, Sk, D, int(bool(causal)), qks, sms, st)
+    return dq, dk, dv
+
+
+class FlashAttention_2_BF16_autograd_function(Function):
+    """bf16:16-85: forward in bf16 (returns O fp32, lse fp32), backward in fp32-accumulated MFMA."""
+
+    @staticmethod
+    def forward(q_fp16, k_fp16, v_bf16, causal):
+        return helion_atten_bf16_fwd_training(q_fp16, k_fp16, v_bf16, causal)
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        q_fp16, k_fp16, v_bf16, causal = inputs
+        O_fp32, lse_fp32 = output
+        ctx.mark_non_differentiable(lse_fp32)  # bf16:55
+        ctx.save_for_backward(q_fp16, k_fp16, v_bf16, O_fp32, lse_fp32)  # bf16:56
+        ctx.args = causal
+
+    @staticmethod
+    def backward(ctx, dO, _lse):
+        q_fp16, k_fp16, v_bf16, O_fp32, lse_fp32 = ctx.saved_tensors
+        causal = ctx.args
+        if dO is None:
+            dO = torch.zeros_like(O_fp32)
+        dq, dk, dv = helion_flash_atten_2_algo_4_bwd(q_fp16, k_fp16, v_bf16, O_fp32, lse_fp32,
+                                                     causal, dO)
+        return dq, dk, dv, None  # bf16:85
+
+
+def flash_atten_2_bf16(q_fp16, k_fp16, v_bf16, causal):
+    """bf16:87-105: returns O fp32."""
+    o_fp32, _lse_fp32 = FlashAttention_2_BF16_autograd_function.apply(q_fp16, k_fp16, v_bf16, causal)
+    return o_fp32

@@ -1,0 +1,180 @@
+"""Drop-in for ``attention_int8`` of selau642/QuantizedAttention, backed by gfx950 HIP kernels.
+
+Public names (same signatures, argument meaning, outputs and assertion messages):
+  SageAttention3_Int8_autograd_function   attention_int8.py:20-95
+  helion_atten_int8_hl_dot_fwd            attention_int8.py:97-262
+  helion_atten_int8_hl_dot_bwd            attention_int8.py:264-432
+  sage_attention_3_int8                   attention_int8.py:434-451
+  baseline_pytorch_attention              attention_int8.py:453-481
+
+Semantics follow the build contract of SURVEY.md §8a (rows A4-A6): attention per (batch, head)
+(F2), corrected backward (F4), SageAttention k-smoothing with the token mean (F1).  The
+``helion_*`` names are kept for drop-in compatibility; no Helion/Triton is involved.
+"""
+from __future__ import annotations
+
+import math
+from typing import Tuple
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+from ._baseline import baseline_pytorch_attention  # noqa: F401  (re-exported like the reference)
+
+BQ = 32   # Bq  (register_tunable default, int8:155)
+BKV = 32  # Bkv (int8:158)
+
+__all__ = [
+    "SageAttention3_Int8_autograd_function", "helion_atten_int8_hl_dot_fwd",
+    "helion_atten_int8_hl_dot_bwd", "sage_attention_3_int8", "baseline_pytorch_attention",
+]
+
+
+def _qk_scale(head_dim: int) -> float:
+    return 1.0 / math.sqrt(head_dim) * 1.44269504  # int8:151-153
+
+
+def _check_shapes(q, k, v):
+    batch, head, q_tokens, q_head_dim = q.shape
+    _, _, k_tokens, k_head_dim = k.shape
+    _, _, v_tokens, v_head_dim = v.shape
+    assert k_tokens == v_tokens, "k and v tokens are different"
+    assert k_head_dim == v_head_dim, "k head_dim and v head_dim are different"
+    if q_tokens != k_tokens or q_head_dim != k_head_dim or q.shape[:2] != k.shape[:2] \
+            or k.shape[:2] != v.shape[:2]:
+        raise _lib.QAttnError("qattn int8: q/k/v must share (batch, head, tokens, head_dim)")
+    if q_tokens % BQ != 0:
+        raise _lib.QAttnError(f"qattn int8: tokens must be a multiple of {BQ}")
+    if q_head_dim not in (64, 128):
+        raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
+
+
+def _int8_forward(q, k, v, smooth: bool):
+    _check_shapes(q, k, v)
+    _lib.require_gpu(q, k, v)
+    q = q.to(torch.float16).contiguous()
+    k = k.to(torch.float16).contiguous()
+    v = v.to(torch.float16).contiguous()
+    B, H, S, D = q.shape
+    N = B * H * S
+    dev = q.device
+    st = _lib.stream_of(q)
+    q_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
+    k_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
+    v_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
+    sq = torch.empty((N // BQ,), dtype=torch.float16, device=dev)
+    sk = torch.empty((N // BKV,), dtype=torch.float16, device=dev)
+    sv = torch.empty((N // BKV,), dtype=torch.float16, device=dev)
+    vdq = torch.empty((N, D), dtype=torch.float16, device=dev)  # workspace fp16(v_i8 * sv)
+    O = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
+    lse = torch.empty((N,), dtype=torch.float16, device=dev)
+    k_mean = None
+    if smooth:
+        k_mean = torch.empty((B, H, 1, D), dtype=torch.float16, device=dev)
+        _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(k_mean), B * H, S, D, st)
+    _lib.call("qattn_int8_quant", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), None, None, N, S, D, st)
+    _lib.call("qattn_int8_quant", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None,
+              _lib.ptr(k_mean), N, S, D, st)
+    _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vdq), None,
+              N, S, D, st)
+    _lib.call("qattn_int8_attn_fwd", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
+              _lib.ptr(vdq), _lib.ptr(O), _lib.ptr(lse), B * H, S, D,
+              float(torch.tensor(_qk_scale(D), dtype=torch.float32)), st)
+    # k_i8T is returned as the [D, N] view of the row-major [N, D] tensor (same values/shape as
+    # int8:165, zero-copy).
+    return O, lse, q_i8, k_i8.t(), v_i8, sq, sk, sv, k_mean
+
+
+def helion_atten_int8_hl_dot_fwd(
+    q_fp16_input: torch.Tensor,
+    k_fp16_input: torch.Tensor,
+    v_fp16_input: torch.Tensor,
+) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
+           torch.Tensor, torch.Tensor, torch.Tensor, int, int]:
+    """int8 forward (int8:101-262): returns (O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv)."""
+    O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, _ = _int8_forward(
+        q_fp16_input, k_fp16_input, v_fp16_input, smooth=False)
+    return O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, BQ, BKV
+
+
+def helion_atten_int8_hl_dot_bwd(
+    dO_input_fp16: torch.Tensor,
+    q_bh_int8: torch.Tensor,
+    sq_bh_fp16: torch.Tensor,
+    k_bh_int8_T: torch.Tensor,
+    k_mean_bh_fp16: torch.Tensor,
+    sk_bh_fp16: torch.Tensor,
+    v_bh_int8: torch.Tensor,
+    sv_bh_fp16: torch.Tensor,
+    O_input_fp16: torch.Tensor,
+    lse_input_fp16: torch.Tensor,
+    Bq: int,
+    Bkv: int,
+) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Corrected int8 backward (int8:268-432): returns fp16 (dq, dk, dv) [B,H,S,D].
+
+    k_mean is accepted for signature compatibility; its term multiplies rowsum(dS) = 0 and is
+    dropped (build contract).
+    """
+    if Bq != BQ or Bkv != BKV:
+        raise _lib.QAttnError("qattn int8 backward is built for Bq = Bkv = 32")
+    O = O_input_fp16.to(torch.float16).contiguous()
+    dO = dO_input_fp16.to(torch.float16).contiguous()
+    _lib.require_gpu(dO, O, q_bh_int8)
+    B, H, S, D = O.shape
+    N = B * H * S
+    dev = O.device
+    st = _lib.stream_of(O)
+    k_i8 = k_bh_int8_T.t().contiguous()  # [N, D] (a no-op for the view our forward returns)
+    q_i8 = q_bh_int8.contiguous()
+    v_i8 = v_bh_int8.contiguous()
+    dO_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
+    sdO = torch.empty((N // BQ,), dtype=torch.float16, device=dev)
+    Drow = torch.empty((N,), dtype=torch.float32, device=dev)
+    _lib.call("qattn_int8_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(dO_i8), _lib.ptr(sdO),
+              _lib.ptr(Drow), B * H, S, D, st)
+    dq = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
+    dk = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
+    dv = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
+    qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
+    sms = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
+    _lib.call("qattn_int8_attn_bwd", _lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8),
+              _lib.ptr(sq_bh_fp16.contiguous()), _lib.ptr(k_i8), _lib.ptr(sk_bh_fp16.contiguous()),
+              _lib.ptr(v_i8), _lib.ptr(sv_bh_fp16.contiguous()), _lib.ptr(lse_input_fp16.contiguous()),
+              _lib.ptr(Drow), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), None, None, None,
+              B * H, S, D, qks, sms, st)
+    return dq, dk, dv
+
+
+class SageAttention3_Int8_autograd_function(Function):
+    """int8:20-95.  forward(q, k, v) -> 11-tuple
+    (O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv)."""
+
+    @staticmethod
+    def forward(q_fp16, k_fp16, v_fp16):
+        O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean = _int8_forward(q_fp16, k_fp16, v_fp16,
+                                                                      smooth=True)
+        return O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, BQ, BKV
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv = output
+        ctx.mark_non_differentiable(lse, k_mean, sq, sk, sv)  # int8:52-56
+        ctx.save_for_backward(O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv)  # int8:58-64
+        ctx.args = (Bq, Bkv)
+
+    @staticmethod
+    def backward(ctx, dO_fp16, _lse, _k_mean, _q_i8, _k_i8T, _v_i8, _sq, _sk, _sv, _Bq, _Bkv):
+        O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv = ctx.saved_tensors
+        Bq, Bkv = ctx.args
+        if dO_fp16 is None:
+            dO_fp16 = torch.zeros_like(O)
+        dq, dk, dv = helion_atten_int8_hl_dot_bwd(dO_fp16, q_i8, sq, k_i8T, k_mean, sk, v_i8, sv,
+                                                   O, lse, Bq, Bkv)
+        return dq, dk, dv
+
+
+def sage_attention_3_int8(q_fp16, k_fp16, v_fp16):
+    """int8:434-451: SageAttention3 int8 attention with autograd; returns O fp16."""
+    return SageAttention3_Int8_autograd_function.apply(q_fp16, k_fp16, v_fp16)[0]

@@ -1,0 +1,65 @@
+"""Build libqattn.so (all HIP kernels + the C-ABI) in-tree for gfx950.
+
+Plain hipcc, no torch headers: the library is a C-ABI boundary (include/qattn.h) that any host
+(ctypes here) binds.  Objects are rebuilt when a source or header is newer than the object.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "_build"
+LIB = PKG / "libqattn.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+CFLAGS = [
+    "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+    "-fhip-fp32-correctly-rounded-divide-sqrt",  # the quantiser needs IEEE fp32 division
+    "-fno-gpu-rdc", "-Wno-unused-result",
+]
+
+
+def _compile(src: Path, obj: Path) -> str:
+    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
+    return src.name
+
+
+def build(verbose: bool = True, jobs: int = 8) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    headers = list(CSRC.glob("*.h"))
+    hdr_mtime = max((h.stat().st_mtime for h in headers), default=0.0)
+    srcs = sorted(CSRC.glob("*.hip"))
+    todo = []
+    objs = []
+    for s in srcs:
+        o = BUILD / (s.stem + ".o")
+        objs.append(o)
+        if not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr_mtime):
+            todo.append((s, o))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            for name in ex.map(lambda so: _compile(*so), todo):
+                if verbose:
+                    print(f"[qattn build] compiled {name}", file=sys.stderr)
+    if todo or not LIB.exists() or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        tmp = LIB.with_suffix(".so.tmp")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, LIB)
+        if verbose:
+            print(f"[qattn build] linked {LIB}", file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build()

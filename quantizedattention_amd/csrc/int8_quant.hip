@@ -1,0 +1,134 @@
+// SageAttention-3 per-block int8 quantiser (replaces the quantisation inside
+// helion_atten_int8_hl_dot_fwd, attention_int8.py:178-195 and 241-247) and the k-smoothing mean
+// (build contract for attention_int8.py:24-25).
+//
+// Numerics (bit-exact with the eager reference):
+//   s   = RNE_fp16( fp32(amax|X|) / 127 )            (IEEE fp32 divide)
+//   idx = trunc( RNE_fp16( fp32(x) / fp32(s) ) )      (IEEE fp32 divide, fp16 round, then trunc)
+// An all-zero block (s == 0) yields idx 0.
+//
+// HBM-bound: one wave per 32-token block (32 x D fp16 = 8 KB for D=128), 16-byte loads/stores,
+// fully coalesced (1 KiB per wave instruction in, 512 B out).
+#include "common.h"
+
+namespace qattn {
+
+// rows: total rows (multiple of 32); rows_per_head: S (for the k-mean lookup)
+template <int D, bool DEQ, bool SMOOTH>
+__global__ __launch_bounds__(256) void quant_block32_kernel(
+    const _Float16* __restrict__ x, int8_t* __restrict__ idx, _Float16* __restrict__ scale,
+    _Float16* __restrict__ deq, const _Float16* __restrict__ kmean, long nblocks, int rows_per_head) {
+  constexpr int ELEMS = 32 * D;        // elements per block
+  constexpr int ITERS = ELEMS / 512;   // 8 halfs per lane per iteration
+  const int lane = threadIdx.x & 63;
+  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= nblocks) return;
+  const _Float16* xb = x + blk * ELEMS;
+  v8h v[ITERS];
+  const _Float16* km = nullptr;
+  if constexpr (SMOOTH) km = kmean + (blk * 32 / rows_per_head) * D;
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int e = (i * 64 + lane) * 8;
+    v[i] = *reinterpret_cast<const v8h*>(xb + e);
+    if constexpr (SMOOTH) {
+      const int d0 = e % D;
+      const v8h m = *reinterpret_cast<const v8h*>(km + d0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = (_Float16)((float)v[i][j] - (float)m[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf((float)v[i][j]));
+  }
+  amax = wave_max_f(amax);
+  const _Float16 s16 = (_Float16)(amax / 127.0f);
+  const float s = (float)s16;
+  if (lane == 0) scale[blk] = s16;
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int e = (i * 64 + lane) * 8;
+    unsigned lo = 0, hi = 0;
+    v8h dq;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int qi = 0;
+      if (s != 0.f) qi = (int)__builtin_truncf((float)(_Float16)((float)v[i][j] / s));
+      const unsigned b = (unsigned)(qi & 0xff);
+      if (j < 4) lo |= b << (8 * j); else hi |= b << (8 * (j - 4));
+      if constexpr (DEQ) dq[j] = (_Float16)((float)qi * s);
+    }
+    *reinterpret_cast<v2u*>(idx + blk * ELEMS + e) = v2u{lo, hi};
+    if constexpr (DEQ) *reinterpret_cast<v8h*>(deq + blk * ELEMS + e) = dq;
+  }
+}
+
+// k_mean[bh][d] = fp16( sum_s fp32(k[bh][s][d]) / S )   (eager `k.mean(-2)` in fp16, fp32 accumulate)
+template <int D>
+__global__ __launch_bounds__(256) void kmean_kernel(const _Float16* __restrict__ k,
+                                                    _Float16* __restrict__ kmean, int S) {
+  constexpr int TPR = D / 8;           // threads per row (8 halfs each)
+  constexpr int RPI = 256 / TPR;       // rows per iteration
+  __shared__ float part[RPI][D + 1];
+  const int bh = blockIdx.x;
+  const int t = threadIdx.x;
+  const int c = (t % TPR) * 8, r0 = t / TPR;
+  const _Float16* kb = k + (long)bh * S * D;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < S; r += RPI) {
+    const v8h x = *reinterpret_cast<const v8h*>(kb + (long)r * D + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += (float)x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[r0][c + j] = acc[j];
+  __syncthreads();
+  if (t < D) {
+    float s = 0.f;
+    for (int r = 0; r < RPI; ++r) s += part[r][t];
+    kmean[(long)bh * D + t] = (_Float16)(s / (float)S);
+  }
+}
+
+}  // namespace qattn
+
+using namespace qattn;
+
+extern "C" int qattn_int8_quant(const void* x, void* idx, void* scale, void* deq, const void* kmean,
+                                long rows, int rows_per_head, int head_dim, void* stream) {
+  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  if (kmean && rows_per_head % 32 != 0) return 1;
+  const long nblocks = rows / 32;
+  if (nblocks == 0) return 0;
+  dim3 grid((unsigned)((nblocks + 3) / 4)), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  auto X = (const _Float16*)x;
+  auto I = (int8_t*)idx;
+  auto Sc = (_Float16*)scale;
+  auto Q = (_Float16*)deq;
+  auto M = (const _Float16*)kmean;
+#define QA_LAUNCH(Dv, DQ, SM) \
+  hipLaunchKernelGGL((quant_block32_kernel<Dv, DQ, SM>), grid, block, 0, st, X, I, Sc, Q, M, nblocks, rows_per_head)
+  if (head_dim == 128) {
+    if (deq) { if (kmean) QA_LAUNCH(128, true, true); else QA_LAUNCH(128, true, false); }
+    else { if (kmean) QA_LAUNCH(128, false, true); else QA_LAUNCH(128, false, false); }
+  } else {
+    if (deq) { if (kmean) QA_LAUNCH(64, true, true); else QA_LAUNCH(64, true, false); }
+    else { if (kmean) QA_LAUNCH(64, false, true); else QA_LAUNCH(64, false, false); }
+  }
+#undef QA_LAUNCH
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_kmean(const void* k, void* kmean, long bh, long seq, int head_dim, void* stream) {
+  if (head_dim != 64 && head_dim != 128) return 1;
+  if (bh == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (head_dim == 128)
+    hipLaunchKernelGGL((kmean_kernel<128>), dim3((unsigned)bh), dim3(256), 0, st, (const _Float16*)k,
+                       (_Float16*)kmean, (int)seq);
+  else
+    hipLaunchKernelGGL((kmean_kernel<64>), dim3((unsigned)bh), dim3(256), 0, st, (const _Float16*)k,
+                       (_Float16*)kmean, (int)seq);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -1,0 +1,65 @@
+// Fragment-layout probes: one-wave GEMM tiles that load operands with the lane maps assumed in
+// common.h and store C with the assumed C/D map.  tests/test_gpu_layout.py checks them against a
+// CPU matmul on asymmetric integer data (cdna_hip_programming.md §3: "A=I-check with ASYMMETRIC B").
+#include "common.h"
+
+namespace qattn {
+
+// C[32x32] (i32, row-major) = A[32x32] (i8, row-major [m][k]) * B[32x32] (i8, row-major [k][n])
+__global__ void probe_mfma_i8_kernel(const int8_t* A, const int8_t* B, int* C) {
+  const int l = threadIdx.x, h = l >> 5, c = l & 31;
+  v4i a, b;
+  int8_t* ap = reinterpret_cast<int8_t*>(&a);
+  int8_t* bp = reinterpret_cast<int8_t*>(&b);
+  for (int j = 0; j < 16; ++j) {
+    ap[j] = A[c * 32 + 16 * h + j];
+    bp[j] = B[(16 * h + j) * 32 + c];
+  }
+  v16i acc = mfma_i8(a, b, v16i{});
+  for (int r = 0; r < 16; ++r) C[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + c] = acc[r];
+}
+
+// C[32x32] (f32) = A[32x16] (f16 [m][k]) * B[16x32] (f16 [k][n])
+__global__ void probe_mfma_f16_kernel(const _Float16* A, const _Float16* B, float* C) {
+  const int l = threadIdx.x, h = l >> 5, c = l & 31;
+  v8h a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = A[c * 16 + 8 * h + j];
+    b[j] = B[(8 * h + j) * 32 + c];
+  }
+  v16f acc = mfma_f16(a, b, v16f{});
+  for (int r = 0; r < 16; ++r) C[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + c] = acc[r];
+}
+
+// ds_read_b64_tr_b16 probe: M [16 rows][64 cols] u16 in LDS (row-major, 128 B rows); lane l of
+// group g reads the 4x16 block rows 4*(g&3).. , cols 16*(g)...; output [64 lanes][4].
+__global__ void probe_tr16_kernel(const unsigned short* M, unsigned short* out) {
+  __shared__ __attribute__((aligned(16))) unsigned short lds[16 * 64];
+  const int l = threadIdx.x;
+  for (int i = l; i < 16 * 64; i += 64) lds[i] = M[i];
+  __syncthreads();
+  const int g = l >> 4, i = l & 15;
+  const int row = 4 * g + (i >> 2), col = 16 * g + 4 * (i & 3);
+  v4s r = ds_read_tr16(&lds[row * 64 + col]);
+  for (int j = 0; j < 4; ++j) out[l * 4 + j] = (unsigned short)r[j];
+}
+
+}  // namespace qattn
+
+using namespace qattn;
+
+extern "C" int qattn_probe_mfma_i8(const void* A, const void* B, void* C, void* stream) {
+  hipLaunchKernelGGL(probe_mfma_i8_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (const int8_t*)A, (const int8_t*)B, (int*)C);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+extern "C" int qattn_probe_mfma_f16(const void* A, const void* B, void* C, void* stream) {
+  hipLaunchKernelGGL(probe_mfma_f16_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (const _Float16*)A, (const _Float16*)B, (float*)C);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+extern "C" int qattn_probe_tr16(const void* M, void* out, void* stream) {
+  hipLaunchKernelGGL(probe_tr16_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (const unsigned short*)M, (unsigned short*)out);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -1,0 +1,44 @@
+"""MFMA / ds_read_tr16 fragment-map probes (the lane maps common.h assumes), asymmetric integer data."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_mfma_i8_layout(lib):
+    from quantizedattention_amd import _lib
+    g = torch.Generator().manual_seed(1)
+    A = torch.randint(-100, 100, (32, 32), generator=g, dtype=torch.int8)
+    B = torch.randint(-100, 100, (32, 32), generator=g, dtype=torch.int8)
+    Ad, Bd = A.cuda(), B.cuda()
+    C = torch.empty((32, 32), dtype=torch.int32, device="cuda")
+    _lib.call("qattn_probe_mfma_i8", _lib.ptr(Ad), _lib.ptr(Bd), _lib.ptr(C), _lib.stream_of(C))
+    ref = (A.long() @ B.long()).int()
+    assert torch.equal(C.cpu(), ref)
+
+
+def test_mfma_f16_layout(lib):
+    from quantizedattention_amd import _lib
+    g = torch.Generator().manual_seed(2)
+    A = torch.randint(-8, 8, (32, 16), generator=g).half()
+    B = torch.randint(-8, 8, (16, 32), generator=g).half()
+    Ad, Bd = A.cuda(), B.cuda()  # keep the device copies alive until the kernel has run
+    C = torch.empty((32, 32), dtype=torch.float32, device="cuda")
+    _lib.call("qattn_probe_mfma_f16", _lib.ptr(Ad), _lib.ptr(Bd), _lib.ptr(C), _lib.stream_of(C))
+    torch.cuda.synchronize()
+    assert torch.equal(C.cpu(), A.float() @ B.float())
+
+
+def test_ds_read_tr16(lib):
+    from quantizedattention_amd import _lib
+    M = torch.arange(16 * 64, dtype=torch.int32).to(torch.int16).reshape(16, 64)
+    out = torch.empty((64, 4), dtype=torch.int16, device="cuda")
+    Md = M.cuda()
+    _lib.call("qattn_probe_tr16", _lib.ptr(Md), _lib.ptr(out), _lib.stream_of(out))
+    torch.cuda.synchronize()
+    exp = torch.empty((64, 4), dtype=torch.int16)
+    for l in range(64):
+        g, i = l >> 4, l & 15
+        for q in range(4):
+            exp[l, q] = M[4 * g + q, 16 * g + i]
+    assert torch.equal(out.cpu(), exp)
