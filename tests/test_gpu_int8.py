@@ -83,3 +83,50 @@ def test_int8_fwd_large_size_properties(lib):
                      v[b:b + 1, hh:hh + 1].cpu())
     err = (out[0][b, hh].float().cpu() - ref[0][0, 0].float()).abs().max().item()
     assert err <= 1e-2, err
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.parametrize("shape", [(1, 2, 128, 64), (1, 2, 256, 128), (2, 2, 192, 128), (1, 4, 512, 128)])
+def test_int8_bwd_matches_oracle(lib, shape):
+    from quantizedattention_amd.attention_int8 import (helion_atten_int8_hl_dot_bwd,
+                                                       helion_atten_int8_hl_dot_fwd)
+    q, k, v = [t.half() for t in _inputs(shape, seed=31)]
+    dO = torch.randn(shape, generator=torch.Generator().manual_seed(32)).half()
+    out = helion_atten_int8_hl_dot_fwd(q.cuda(), k.cuda(), v.cuda())
+    O, lse, qi, kiT, vi, sq, sk, sv, Bq, Bkv = out
+    dq, dk, dv = helion_atten_int8_hl_dot_bwd(dO.cuda(), qi, sq, kiT, None, sk, vi, sv, O, lse, Bq, Bkv)
+    torch.cuda.synchronize()
+    rq, rk, rv = R.int8_bwd(dO, qi.cpu(), sq.cpu(), kiT.cpu(), None, sk.cpu(), vi.cpu(), sv.cpu(),
+                            O.cpu(), lse.cpu())
+    for name, a, b in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
+        assert a.dtype == torch.float16 and a.shape == shape
+        assert _rel(a.cpu(), b) <= 0.05, (name, _rel(a.cpu(), b))
+    tq, tk, tv = R.attention_grads_truth(q, k, v, dO, False)
+    for name, a, b in (("dq", dq, tq), ("dk", dk, tk), ("dv", dv, tv)):
+        assert _rel(a.cpu(), b) <= 0.15, (name, _rel(a.cpu(), b))
+
+
+def test_sage_attention_autograd(lib):
+    """sage_attention_3_int8 end to end: smoothing forward + corrected int8 backward."""
+    from quantizedattention_amd.attention_int8 import (SageAttention3_Int8_autograd_function,
+                                                       sage_attention_3_int8)
+    shape = (2, 2, 256, 64)
+    q, k, v = [t.half() for t in _inputs(shape, seed=41)]
+    k = k + 3.0  # a large shared key offset: smoothing removes it without changing softmax
+    qd, kd, vd = (t.cuda().requires_grad_(True) for t in (q, k, v))
+    out = sage_attention_3_int8(qd, kd, vd)
+    outs = SageAttention3_Int8_autograd_function.apply(qd, kd, vd)
+    assert len(outs) == 11 and outs[2].shape == (2, 2, 1, 64) and outs[9] == 32
+    ks, km = R.k_smooth(k)
+    ref = R.int8_fwd(q, ks, v)
+    assert (out.float().cpu() - ref[0].float()).abs().max().item() <= 1e-2
+    assert torch.equal(outs[2].cpu(), km)
+    gt = torch.randn(shape, generator=torch.Generator().manual_seed(42))
+    torch.nn.functional.mse_loss(out.float(), gt.cuda()).backward()
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    torch.nn.functional.mse_loss(R.baseline_pytorch_attention(qf, kf, vf, 64, False), gt).backward()
+    for a, b in ((qd.grad, qf.grad), (kd.grad, kf.grad), (vd.grad, vf.grad)):
+        assert _rel(a.cpu(), b) <= 0.15
