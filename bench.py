@@ -1,0 +1,267 @@
+"""Headline benchmark: fused-attention fwd+bwd at (B,H,S,D) = (4,32,4096,128), int8 vs bf16.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (multi-GPU)
+
+A step = one training pass of the attention operator over one synthetic batch:
+  int8 (the reported `value`): sage_attention_3_int8 forward (k-mean + q/k/v quantisation +
+  int8 attention) and its backward (dO quantisation + D + dK/dV + dQ kernels);
+  bf16 (reported beside it): flash_atten_2_bf16 forward + backward.
+With N > 1 ranks each rank owns its own (4,32,4096,128) shard of a (4N,32,4096,128) batch (weak
+scaling, batch x head sharding) and the step also all-gathers O over RCCL, issued asynchronously
+after the forward so it overlaps the backward.  Inputs are resident in HBM before timing starts.
+
+Prints ONE JSON line (rank 0).  FLOP accounting: fwd 4*BH*S^2*D, bwd 10*BH*S^2*D.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from quantizedattention_amd import _lib  # noqa: E402
+from quantizedattention_amd.attention_bf16 import (  # noqa: E402
+    helion_atten_bf16_fwd_training, helion_flash_atten_2_algo_4_bwd)
+from quantizedattention_amd.attention_int8 import (  # noqa: E402
+    _int8_forward, helion_atten_int8_hl_dot_bwd)
+
+PEAK_I8 = 256 * 8192 * 2.4e9          # ops/s, dense int8 MFMA (MI355X_MICROARCH: 2x bf16 per clock)
+PEAK_BF16 = 256 * 4096 * 2.4e9        # flop/s, dense bf16/fp16 MFMA
+PEAK_HBM = 8.0e12                     # B/s
+
+
+def _f32(x):
+    return float(torch.tensor(x, dtype=torch.float32))
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--shape", type=str, default="4,32,4096,128")
+    p.add_argument("--no-gather", action="store_true", help="skip the O all-gather for N>1")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--skip-bf16", action="store_true")
+    return p.parse_args()
+
+
+def timed(fn, steps, warmup, world):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = (time.perf_counter() - t0) / steps
+    if world > 1:
+        tt = torch.tensor([t], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = tt.item()
+    return t
+
+
+def event_time(fn, n):
+    """Average device time of fn() on the current stream (HIP events), ms."""
+    s = torch.cuda.current_stream()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    a.record(s)
+    for _ in range(n):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / n
+
+
+def int8_kernel_times(q, k, v, dO, n):
+    """Per-kernel average durations (ms) of the int8 path, each launched alone on the stream."""
+    B, H, S, D = q.shape
+    N = B * H * S
+    dev = q.device
+    st = _lib.stream_of(q)
+    P = _lib.ptr
+    e = lambda *shape, dt: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
+    qi, ki, vi, dOi = (e(N, D, dt=torch.int8) for _ in range(4))
+    sq, sk, sv, sdO = (e(N // 32, dt=torch.float16) for _ in range(4))
+    vdq = e(N, D, dt=torch.float16)
+    km = e(B * H, D, dt=torch.float16)
+    O = e(B, H, S, D, dt=torch.float16)
+    lse = e(N, dt=torch.float16)
+    Dr = e(N, dt=torch.float32)
+    dq, dk, dv = (e(B, H, S, D, dt=torch.float16) for _ in range(3))
+    qks, sms = _f32(1 / math.sqrt(D) * 1.44269504), _f32(1 / math.sqrt(D))
+    calls = {
+        "kmean_kernel": lambda: _lib.call("qattn_kmean", P(k), P(km), B * H, S, D, st),
+        "quant_block32_kernel(k)": lambda: _lib.call("qattn_int8_quant", P(k), P(ki), P(sk), None,
+                                                     P(km), N, S, D, st),
+        "quant_block32_kernel(q)": lambda: _lib.call("qattn_int8_quant", P(q), P(qi), P(sq), None,
+                                                     None, N, S, D, st),
+        "quant_block32_kernel(v)": lambda: _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq),
+                                                     None, N, S, D, st),
+        "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk),
+                                                  P(vdq), P(O), P(lse), B * H, S, D, qks, st),
+        "int8_bwd_prep": lambda: _lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(dOi), P(sdO), P(Dr),
+                                           B * H, S, D, st),
+        "int8_bwd_dkdv_kernel": lambda: _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi), P(sq),
+                                                  P(ki), P(sk), P(vi), P(sv), P(lse), P(Dr), P(dk),
+                                                  P(dv), B * H, S, D, qks, sms, st),
+        "int8_bwd_dq_kernel": lambda: _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq),
+                                                P(ki), P(sk), P(vi), P(sv), P(lse), P(Dr), P(dq),
+                                                B * H, S, D, qks, sms, st),
+    }
+    order = list(calls)
+    for name in order:  # populate every buffer once in dependency order
+        calls[name]()
+    return {name: event_time(calls[name], n) for name in order}
+
+
+def cpu_baseline(S, D, seconds):
+    """The reference's eager fp32 path (baseline_pytorch_attention fwd + autograd bwd, restated in
+    oracle/restate.py) on the host cores, one (S, D) head at a time until `seconds` elapse."""
+    from oracle import restate as R
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    heads, t_total = 0, 0.0
+    while t_total < seconds or heads < 2:
+        q, k, v, dO = (torch.randn((1, 1, S, D), generator=g) for _ in range(4))
+        t0 = time.perf_counter()
+        R.attention_grads_truth(q, k, v, dO, False)
+        t_total += time.perf_counter() - t0
+        heads += 1
+        if heads >= 64:
+            break
+    flop = 14.0 * S * S * D * heads
+    return {"value": flop / t_total / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
+            "sample": f"{heads} heads of (S,D)=({S},{D}) fwd+bwd fp32 eager (baseline_pytorch_attention"
+                      f" + autograd), {t_total:.1f} s; scales linearly in B*H"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, H, S, D = (int(x) for x in a.shape.split(","))
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    q, k, v = (torch.randn((B, H, S, D), device=dev, generator=g).half() for _ in range(3))
+    dO = (torch.randn((B, H, S, D), device=dev, generator=g) * 1e-3).half()
+    gather = world > 1 and not a.no_gather
+    O_full = torch.empty((world * B * H, S, D), dtype=torch.float16, device=dev) if gather else None
+    comm = torch.cuda.Stream(device=dev) if gather else None
+
+    def step_int8():
+        O, lse, qi, kiT, vi, sq, sk, sv, km = _int8_forward(q, k, v, smooth=True)
+        work = None
+        if gather:
+            comm.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(comm):
+                work = dist.all_gather_into_tensor(O_full, O.view(B * H, S, D), async_op=True)
+        helion_atten_int8_hl_dot_bwd(dO, qi, sq, kiT, km, sk, vi, sv, O, lse, 32, 32)
+        if work is not None:
+            work.wait()
+            torch.cuda.current_stream().wait_stream(comm)
+
+    flop_fb = 14.0 * B * H * S * S * D
+    t_i8 = timed(step_int8, a.steps, a.warmup, world)
+    res_bf = None
+    if not a.skip_bf16:
+        qb, kb, vb = q, k, v.bfloat16()
+        dOf = dO.float()
+        O32_full = torch.empty((world * B * H, S, D), dtype=torch.float32, device=dev) if gather else None
+
+        def step_bf16():
+            O, lse = helion_atten_bf16_fwd_training(qb, kb, vb, False)
+            work = None
+            if gather:
+                comm.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(comm):
+                    work = dist.all_gather_into_tensor(O32_full, O.view(B * H, S, D), async_op=True)
+            helion_flash_atten_2_algo_4_bwd(qb, kb, vb, O, lse, False, dOf)
+            if work is not None:
+                work.wait()
+                torch.cuda.current_stream().wait_stream(comm)
+
+        t_bf = timed(step_bf16, max(3, a.steps // 2), a.warmup, world)
+        res_bf = {"value": world * flop_fb / t_bf / 1e12, "unit": "TFLOP/s",
+                  "ms_per_step": t_bf * 1e3, "frac_of_bf16_peak": flop_fb / t_bf / PEAK_BF16}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    kt = int8_kernel_times(q, k, v, dO, max(3, a.steps // 2))
+    per_call = {  # algorithmic MFMA work per launch
+        "int8_attn_fwd_kernel": 4.0 * B * H * S * S * D,   # QK^T, PV
+        "int8_bwd_dkdv_kernel": 8.0 * B * H * S * S * D,   # S, dP, dV, dK
+        "int8_bwd_dq_kernel": 6.0 * B * H * S * S * D,     # S, dP (recomputed), dQ
+    }
+    dom = max(per_call, key=lambda n: kt[n])
+    achieved = per_call[dom] / (kt[dom] * 1e-3) / 1e12
+    fwd_ms = sum(v for n, v in kt.items() if not n.startswith("int8_bwd"))
+    out = {
+        "metric": "fused-attn fwd+bwd TFLOP/s & us/call at (B,H,S,D)=(4,32,4096,128), int8 vs bf16",
+        "value": world * flop_fb / t_i8 / 1e12,
+        "unit": "TFLOP/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": t_i8 * 1e3,
+        "us_per_call": t_i8 * 1e6,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic (seeded randn q,k,v fp16; dO = 1e-3*randn fp16)",
+        "config": {"workload": "int8 SageAttention-3 fwd+bwd per rank, non-causal",
+                   "shape_per_rank": [B, H, S, D], "global_batch": B * world,
+                   "parallelism": f"batch x head shard over {world} GPU(s)"
+                                  + (" + async RCCL all-gather of O" if gather else "")},
+        "bf16": res_bf,
+        "int8_fwd": {"ms": fwd_ms, "TOPS": 4.0 * B * H * S * S * D / (fwd_ms * 1e-3) / 1e12,
+                     "frac_of_int8_peak": 4.0 * B * H * S * S * D / (fwd_ms * 1e-3) / PEAK_I8},
+        "kernel_ms": kt,
+        "roofline": {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": PEAK_I8 / 1e12,
+                     "unit": "TFLOP/s", "frac": achieved * 1e12 / PEAK_I8, "traffic": None},
+    }
+    tr_path = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if os.path.exists(tr_path):
+        try:
+            tr = json.load(open(tr_path))
+            out["roofline"]["traffic"] = tr.get(dom)
+        except Exception:
+            pass
+    if world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(S, D, a.cpu_seconds)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -436,12 +436,12 @@ extern "C" int qattn_int8_bwd_prep(const void* dO, const void* O, void* dO_i8, v
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-extern "C" int qattn_int8_attn_bwd(const void* dO_i8, const void* sdO, const void* q_i8,
-                                   const void* sq, const void* k_i8, const void* sk, const void* v_i8,
-                                   const void* sv, const void* lse, const void* Drow, void* dq,
-                                   void* dk, void* dv, void* ws0, void* ws1, void* ws2, long bh,
-                                   long seq, int head_dim, float qks, float sms, void* stream) {
-  (void)ws0; (void)ws1; (void)ws2;
+// which: 1 = dK/dV kernel, 2 = dQ kernel, 3 = both
+static int int8_bwd_launch(int which, const void* dO_i8, const void* sdO, const void* q_i8,
+                           const void* sq, const void* k_i8, const void* sk, const void* v_i8,
+                           const void* sv, const void* lse, const void* Drow, void* dq, void* dk,
+                           void* dv, long bh, long seq, int head_dim, float qks, float sms,
+                           void* stream) {
   if (seq % 64 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
   if (bh == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
@@ -451,23 +451,54 @@ extern "C" int qattn_int8_attn_bwd(const void* dO_i8, const void* sdO, const voi
     using C = I8BwdCfg<Dv>;                                                                      \
     constexpr int sA = 2 * (2 * C::T8 + 2 * C::T16 + 2 * 32 * 4 + 16);                          \
     constexpr int sB = 2 * (2 * 64 * C::RB8 + 64 * C::RB16 + 16);                               \
-    hipFuncSetAttribute((const void*)int8_bwd_dkdv_kernel<Dv>,                                   \
-                        hipFuncAttributeMaxDynamicSharedMemorySize, sA);                         \
-    hipFuncSetAttribute((const void*)int8_bwd_dq_kernel<Dv>,                                     \
-                        hipFuncAttributeMaxDynamicSharedMemorySize, sB);                         \
-    hipLaunchKernelGGL((int8_bwd_dkdv_kernel<Dv>), dim3((unsigned)(nb * bh)), dim3(256), sA, st,  \
-                       (const int8_t*)dO_i8, (const _Float16*)sdO, (const int8_t*)q_i8,           \
-                       (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,             \
-                       (const int8_t*)v_i8, (const _Float16*)sv, (const _Float16*)lse,            \
-                       (const float*)Drow, (_Float16*)dk, (_Float16*)dv, (int)bh, (int)seq, qks,   \
-                       sms);                                                                     \
-    hipLaunchKernelGGL((int8_bwd_dq_kernel<Dv>), dim3((unsigned)(nb * bh)), dim3(256), sB, st,    \
-                       (const int8_t*)dO_i8, (const _Float16*)sdO, (const int8_t*)q_i8,           \
-                       (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,             \
-                       (const int8_t*)v_i8, (const _Float16*)sv, (const _Float16*)lse,            \
-                       (const float*)Drow, (_Float16*)dq, (int)bh, (int)seq, qks, sms);           \
+    if (which & 1) {                                                                             \
+      hipFuncSetAttribute((const void*)int8_bwd_dkdv_kernel<Dv>,                                 \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, sA);                       \
+      hipLaunchKernelGGL((int8_bwd_dkdv_kernel<Dv>), dim3((unsigned)(nb * bh)), dim3(256), sA,    \
+                         st, (const int8_t*)dO_i8, (const _Float16*)sdO, (const int8_t*)q_i8,     \
+                         (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,           \
+                         (const int8_t*)v_i8, (const _Float16*)sv, (const _Float16*)lse,          \
+                         (const float*)Drow, (_Float16*)dk, (_Float16*)dv, (int)bh, (int)seq,     \
+                         qks, sms);                                                              \
+    }                                                                                            \
+    if (which & 2) {                                                                             \
+      hipFuncSetAttribute((const void*)int8_bwd_dq_kernel<Dv>,                                   \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, sB);                       \
+      hipLaunchKernelGGL((int8_bwd_dq_kernel<Dv>), dim3((unsigned)(nb * bh)), dim3(256), sB, st,  \
+                         (const int8_t*)dO_i8, (const _Float16*)sdO, (const int8_t*)q_i8,         \
+                         (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,           \
+                         (const int8_t*)v_i8, (const _Float16*)sv, (const _Float16*)lse,          \
+                         (const float*)Drow, (_Float16*)dq, (int)bh, (int)seq, qks, sms);         \
+    }                                                                                            \
   }
   if (head_dim == 128) QA_LAUNCH(128) else QA_LAUNCH(64)
 #undef QA_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_int8_attn_bwd(const void* dO_i8, const void* sdO, const void* q_i8,
+                                   const void* sq, const void* k_i8, const void* sk, const void* v_i8,
+                                   const void* sv, const void* lse, const void* Drow, void* dq,
+                                   void* dk, void* dv, void* ws0, void* ws1, void* ws2, long bh,
+                                   long seq, int head_dim, float qks, float sms, void* stream) {
+  (void)ws0; (void)ws1; (void)ws2;
+  return int8_bwd_launch(3, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, lse, Drow, dq, dk, dv, bh, seq,
+                         head_dim, qks, sms, stream);
+}
+
+extern "C" int qattn_int8_bwd_dkdv(const void* dO_i8, const void* sdO, const void* q_i8,
+                                   const void* sq, const void* k_i8, const void* sk, const void* v_i8,
+                                   const void* sv, const void* lse, const void* Drow, void* dk,
+                                   void* dv, long bh, long seq, int head_dim, float qks, float sms,
+                                   void* stream) {
+  return int8_bwd_launch(1, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, lse, Drow, nullptr, dk, dv, bh,
+                         seq, head_dim, qks, sms, stream);
+}
+
+extern "C" int qattn_int8_bwd_dq(const void* dO_i8, const void* sdO, const void* q_i8,
+                                 const void* sq, const void* k_i8, const void* sk, const void* v_i8,
+                                 const void* sv, const void* lse, const void* Drow, void* dq, long bh,
+                                 long seq, int head_dim, float qks, float sms, void* stream) {
+  return int8_bwd_launch(2, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, lse, Drow, dq, nullptr, nullptr,
+                         bh, seq, head_dim, qks, sms, stream);
 }
