@@ -36,7 +36,7 @@ SIGNATURES = {
     "qattn_probe_mfma_i8": [_vp, _vp, _vp, _vp],
     "qattn_probe_mfma_f16": [_vp, _vp, _vp, _vp],
     "qattn_probe_tr16": [_vp, _vp, _vp],
-    "qattn_probe_int8_attn_dbg": [_vp] * 7 + [_c_long, _c_long, _c_float, _vp, _vp],
+    "qattn_probe_pk": [_vp, _vp, _vp, _vp],
 }
 
 _lib = None

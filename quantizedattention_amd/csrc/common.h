@@ -74,6 +74,64 @@ QA_DEVICE float wave_max_f(float x) {
   return x;
 }
 
+// Single-instruction max (hipcc otherwise canonicalises both fmaxf inputs with extra v_max).
+QA_DEVICE float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// Full-wave max via DPP + permlane swaps (no LDS traffic); result in every lane.
+QA_DEVICE float wave_max_dpp(float x) {
+  x = vmax(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true)));
+  x = vmax(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true)));
+  x = vmax(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, true)));
+  x = vmax(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, true)));
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax(__uint_as_float(r2[0]), __uint_as_float(r2[1]));
+}
+// Value of lane l^32 (half-wave exchange without LDS).  v_permlane32_swap vdst, vsrc swaps
+// vdst[32..63] with vsrc[0..31]: with vdst = vsrc = x, lanes 0-31 find x[l+32] in the new vsrc and
+// lanes 32-63 find x[l-32] in the new vdst.
+QA_DEVICE unsigned xor32_swap_u(unsigned x, int lane) {
+  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (lane < 32) ? r[1] : r[0];
+}
+QA_DEVICE float xor32_swap(float x, int lane) {
+  return __uint_as_float(xor32_swap_u(__float_as_uint(x), lane));
+}
+
+// Sum / max over the lane pair (l, l^32), result in both lanes.
+QA_DEVICE float pair_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+QA_DEVICE float pair_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// Packed-half transcendental / rounding helpers on 4 pairs: low halves with the e32 form, then high
+// halves with SDWA writing WORD_1 and preserving WORD_0 (hipcc would otherwise unpack, compute and
+// v_pack_b32_f16).  The SDWA UNUSED_PRESERVE read of a VALU-written destination needs 2 wait
+// states; the 3 independent instructions between each pair provide them (tests/test_gpu_layout.py).
+#define QA_PK4(OP)                                                                              \
+  asm(OP "_e32 %0, %4\n\t" OP "_e32 %1, %5\n\t" OP "_e32 %2, %6\n\t" OP "_e32 %3, %7\n\t"      \
+      OP "_sdwa %0, %4 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"           \
+      OP "_sdwa %1, %5 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"           \
+      OP "_sdwa %2, %6 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"           \
+      OP "_sdwa %3, %7 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1"                 \
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])                                      \
+      : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]))
+QA_DEVICE void exp2_pk4(const v2h* x, v2h* r) { QA_PK4("v_exp_f16"); }
+QA_DEVICE void trunc_pk4(const v2h* x, v2h* r) { QA_PK4("v_trunc_f16"); }
+
+// LDS-DMA of one 16-B chunk per lane: the LDS destination is lds_base (wave-uniform) + 16*lane.
+QA_DEVICE void glds16(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, cols 4p..4p+3 of a 4x16
 // block; lane i receives column i of the 4 rows (cdna_hip_programming.md T10).
 QA_DEVICE v4s ds_read_tr16(const void* lds_addr) {

@@ -2,30 +2,39 @@
 // helion_atten_int8_hl_dot_fwd, attention_int8.py:170-257), per (batch, head).
 //
 // Work decomposition
-//   * one workgroup = 4 waves = 128 query rows of one (b,h); wave w owns rows 32w..32w+31, which is
-//     exactly one 32-token q-quant block (one sq scale per wave);
-//   * keys stream in 64-key blocks (two 32-key Bkv tiles) through a 2-stage LDS ring
-//     (register staging: issue global loads for block j+1, compute block j, write LDS, 1 barrier);
-//   * workgroups of one head are kept on one XCD (K/V of a head stay in that XCD's L2).
+//   * one workgroup = 8 waves = 256 query rows of one (b,h); wave w owns rows 32w..32w+31 = one
+//     32-token q-quant block (one sq scale per wave).  Two waves per SIMD: one wave's softmax VALU
+//     overlaps the other's MFMAs.
+//   * keys stream in 64-key blocks (two 32-key Bkv tiles) through a 2-stage LDS ring filled by
+//     LDS-DMA (global_load_lds_dwordx4: no staging registers; the bank swizzle is applied to the
+//     per-lane source address, the LDS image is written lane-linearly).  One barrier per block.
+//   * every sk scale of the head sits in LDS (loaded once); workgroups of one head share an XCD.
 //
-// Per 32-key tile and wave (the "swapped" orientation: keys in registers, queries on lanes):
-//   S^T[key][q] = K_i8 . Q_i8^T          4 x v_mfma_i32_32x32x32_i8  (D=128)
-//   per-q online softmax in registers (no LDS):
-//     S   = fp16(acc * sq*sk*qks)                         (int8:200-203)
-//     m'  = max(m, rowmax S);  P = exp2(fp16(S - m'))      (int8:205-213)
-//     r   = exp2(fp16(m - m')); l = l*r + sum P; O *= r    (int8:217-225)
-//     sp  = exp2(fp16(rowmax S - m')) / 127; P_i8 = trunc(P / sp)   (int8:232-237)
-//   O^T[d][q] += Vdq^T . (P_i8*sp)^T       8 x v_mfma_f32_32x32x16_f16 (D=128)
-// where Vdq = fp16(v_i8 * sv) is written by the quantiser.  Sum_t sp*sv*(P_i8 . v_i8) of the
-// reference (int8:249-250) is computed exactly up to the fp16 rounding of the two dequantised
-// operands (relative 2^-12 each); the fp32 accumulation then runs inside the MFMA, which removes
-// the per-tile i32->f32 dequantisation of a D-wide accumulator (8 VALU ops per score element).
+// Per 32-key tile and wave (swapped orientation: keys in registers, query on the lane pair l, l^32):
+//   S^T[key][q] = K_i8 . Q_i8^T          D/32 x v_mfma_i32_32x32x32_i8
+//   per-q online softmax in packed fp16 (v_pk_*_f16, v_exp_f16), reference rounding points:
+//     S    = fp16(acc * sq*sk*qks)                       (int8:200-203)
+//     rm   = rowmax S;  m' = max(m, rm)                   (int8:205-209)
+//     e    = exp2(fp16(S - rm))  so that P = e*exp2(rm-m') and P/sp = 127*e   (int8:211,232-236)
+//     r    = exp2(fp16(m - m')); l = l*r + exp2(rm-m') * sum e;  O *= r      (int8:215-225)
+//     P_i8 = trunc(127*e);  operand = fp16(P_i8 * sp), sp = exp2(rm - m')/127  (int8:232-237)
+//   O^T[d][q] += Vdq^T . operand^T        2*D/32 x v_mfma_f32_32x32x16_f16
+// Vdq = fp16(v_i8 * sv) is written by the quantiser, so the fp32 accumulation of
+// sum_t sp*sv*(P_i8 . v_i8) (int8:249-250) runs inside the MFMA: exact up to the fp16 rounding of
+// the two dequantised operands (2^-12 relative each), and the D-wide per-tile i32->f32
+// dequantisation (8 VALU ops per score element) disappears.
+// The int8 accumulator starts at 0x4B400000 (C operand): its bit pattern is then the fp32 number
+// M + acc with M = 1.5 * 2^23 (exact while |acc| < 2^22; |acc| <= D*127^2), so
+// S = fma(bits, c, -M c) needs no i32->f32 convert.  c keeps 22 significant bits so that M*c = 3c*2^22
+// is exact and the fused multiply-add rounds acc*c once, straight to fp16 (v_fma_mix).
 #include "common.h"
 
 namespace qattn {
 
 template <int D>
 struct Int8FwdCfg {
+  static constexpr int WAVES = 4;
+  static constexpr int QROWS = 32 * WAVES;      // query rows per workgroup
   static constexpr int KB = 64;                 // keys per LDS stage
   static constexpr int K_BYTES = KB * D;        // int8 K block
   static constexpr int V_BYTES = KB * D * 2;    // fp16 Vdq block
@@ -36,40 +45,68 @@ struct Int8FwdCfg {
   static constexpr int V_CH = D * 2 / 16;       // 16-B chunks per V row
   static constexpr int K_SW_SHIFT = (D == 128) ? 1 : 2;
   static constexpr int V_SW_SHIFT = (D == 128) ? 2 : 1;
-  static constexpr int K_LOADS = K_BYTES / (256 * 16);   // dwordx4 per thread
-  static constexpr int V_LOADS = V_BYTES / (256 * 16);
+  static constexpr int K_INST = K_BYTES / 1024; // 1-KiB LDS-DMA wave instructions per block
+  static constexpr int V_INST = V_BYTES / 1024;
 };
 
 template <int D>
-QA_DEVICE int k_lds_off(int row, int ch) {
+QA_DEVICE int k_sw(int row) {
   using C = Int8FwdCfg<D>;
-  return row * D + 16 * (ch ^ ((row >> C::K_SW_SHIFT) & (C::K_CH - 1)));
+  return (row >> C::K_SW_SHIFT) & (C::K_CH - 1);
 }
 template <int D>
-QA_DEVICE int v_lds_off(int row, int ch) {
+QA_DEVICE int v_sw(int row) {
   using C = Int8FwdCfg<D>;
-  return row * (2 * D) + 16 * (ch ^ ((row & 3) << C::V_SW_SHIFT));
+  return (row & 3) << C::V_SW_SHIFT;
 }
 
-template <int D, bool DBG = false>
-__global__ __launch_bounds__(256, 2) void int8_attn_fwd_kernel(
+// Issue the LDS-DMA of one 64-key block (rows >= S are clamped to a valid row; never consumed).
+template <int D>
+QA_DEVICE void stage_block(const int8_t* kbase, const _Float16* vbase, char* kl, int key0, int S,
+                           int wave, int lane) {
+  using C = Int8FwdCfg<D>;
+  char* vl = kl + C::K_BYTES;
+  for (int inst = wave; inst < C::K_INST; inst += C::WAVES) {
+    constexpr int RPI = 64 / C::K_CH;
+    const int row = inst * RPI + lane / C::K_CH, p = lane % C::K_CH;
+    const int grow = min(key0 + row, S - 1);
+    glds16(kbase + (long)grow * D + 16 * (p ^ k_sw<D>(row)), kl + inst * 1024);
+  }
+  for (int inst = wave; inst < C::V_INST; inst += C::WAVES) {
+    constexpr int RPI = 64 / C::V_CH;
+    const int row = inst * RPI + lane / C::V_CH, p = lane % C::V_CH;
+    const int grow = min(key0 + row, S - 1);
+    glds16(reinterpret_cast<const char*>(vbase + (long)grow * D) + 16 * (p ^ v_sw<D>(row)),
+           vl + inst * 1024);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
     const _Float16* __restrict__ sk, const _Float16* __restrict__ vdq, _Float16* __restrict__ out,
-    _Float16* __restrict__ lse, int BH, int S, float qks, float* __restrict__ dbg = nullptr) {
+    _Float16* __restrict__ lse, int BH, int S, float qks) {
   using C = Int8FwdCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  _Float16* sk_lds = reinterpret_cast<_Float16*>(smem + 2 * C::STAGE);
 
-  const int nq = (S + 127) / 128;
+  const int nq = (S + C::QROWS - 1) / C::QROWS;
   int bh, qt;
   xcd_remap(blockIdx.x, nq, BH, bh, qt);
   const int tid = threadIdx.x;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int h = lane >> 5;
   const int c32 = lane & 31;
-  const int q0 = qt * 128 + wave * 32;          // first query row of this wave
-  const bool active = q0 < S;                   // wave-uniform
+  const int q0 = qt * C::QROWS + wave * 32;
+  const bool active = q0 < S;
   const long head_row0 = (long)bh * S;
+  const int8_t* kbase = k_i8 + head_row0 * D;
+  const _Float16* vbase = vdq + head_row0 * D;
+  const int nkb = (S + C::KB - 1) / C::KB;
+
+  stage_block<D>(kbase, vbase, smem, 0, S, wave, lane);
+  for (int i = tid; i < S / 32; i += 64 * C::WAVES) sk_lds[i] = sk[head_row0 / 32 + i];
 
   // ---- Q fragment (B operand of S^T = K Q^T): lane holds Q[q0+c32][32s + 16h .. +16]
   v4i qf[C::NKS];
@@ -80,109 +117,93 @@ __global__ __launch_bounds__(256, 2) void int8_attn_fwd_kernel(
     for (int s = 0; s < C::NKS; ++s) qf[s] = *reinterpret_cast<const v4i*>(qrow + 32 * s);
     sqw = (float)sq[(head_row0 + q0) / 32];
   }
+  const float cq = sqw * qks;
+  v16i magic;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) magic[i] = 0x4B400000;
 
   v16f o[C::NDB];
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) o[b] = v16f{};
   _Float16 m = (_Float16)(-INFINITY);
-  float l = 1.0f;
+  float l = 0.f;  // the reference starts at 1.0 and wipes it with r = 0 on the first tile
+  const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
+  const v2h one2 = {(_Float16)1.0f, (_Float16)1.0f};
 
-  const int nkb = (S + C::KB - 1) / C::KB;
-  const int8_t* kbase = k_i8 + head_row0 * D;
-  const _Float16* vbase = vdq + head_row0 * D;
-  const _Float16* skbase = sk + head_row0 / 32;
-
-  // ---- register staging of one 64-key block
-  v4i kst[C::K_LOADS], vst[C::V_LOADS];
-  auto stage_load = [&](int kb) {
-    const int key0 = kb * C::KB;
-#pragma unroll
-    for (int i = 0; i < C::K_LOADS; ++i) {
-      const int e = (i * 256 + tid);            // 16-B chunk index within the block
-      const int row = e / C::K_CH;
-      if (key0 + row < S)
-        kst[i] = *reinterpret_cast<const v4i*>(kbase + (long)(key0 + row) * D + 16 * (e % C::K_CH));
-      else
-        kst[i] = v4i{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int i = 0; i < C::V_LOADS; ++i) {
-      const int e = (i * 256 + tid);
-      const int row = e / C::V_CH;
-      if (key0 + row < S)
-        vst[i] = *reinterpret_cast<const v4i*>(vbase + (long)(key0 + row) * D + 8 * (e % C::V_CH));
-      else
-        vst[i] = v4i{0, 0, 0, 0};
-    }
-  };
-  auto stage_store = [&](int buf) {
-    char* kl = smem + buf * C::STAGE;
-    char* vl = kl + C::K_BYTES;
-#pragma unroll
-    for (int i = 0; i < C::K_LOADS; ++i) {
-      const int e = (i * 256 + tid);
-      *reinterpret_cast<v4i*>(kl + k_lds_off<D>(e / C::K_CH, e % C::K_CH)) = kst[i];
-    }
-#pragma unroll
-    for (int i = 0; i < C::V_LOADS; ++i) {
-      const int e = (i * 256 + tid);
-      *reinterpret_cast<v4i*>(vl + v_lds_off<D>(e / C::V_CH, e % C::V_CH)) = vst[i];
-    }
-  };
-
-  stage_load(0);
-  stage_store(0);
   __syncthreads();
-
   for (int kb = 0; kb < nkb; ++kb) {
-    if (kb + 1 < nkb) stage_load(kb + 1);
+    if (kb + 1 < nkb)
+      stage_block<D>(kbase, vbase, smem + ((kb + 1) & 1) * C::STAGE, (kb + 1) * C::KB, S, wave, lane);
     const char* kl = smem + (kb & 1) * C::STAGE;
     const char* vl = kl + C::K_BYTES;
     const int ntile = min(2, (S - kb * C::KB) / 32);
     if (active) {
-      for (int u = 0; u < ntile; ++u) {
-        // ---------------- S^T = K Q^T (int8 MFMA)
-        v16i acc = v16i{};
+      // ---------------- S^T = K Q^T for both tiles first (independent int8 MFMA chains)
+      v16i acc[2];
 #pragma unroll
-        for (int s = 0; s < C::NKS; ++s) {
-          const v4i kf = *reinterpret_cast<const v4i*>(kl + k_lds_off<D>(32 * u + c32, 2 * s + h));
-          acc = mfma_i8(kf, qf[s], acc);
-        }
-        // ---------------- online softmax + per-row P quantisation (lane = query row)
-        const float skt = (float)skbase[kb * 2 + u];
-        const float cs = (sqw * skt) * qks;
-        _Float16 s16[16];
-        _Float16 rml = (_Float16)(-INFINITY);
+      for (int u = 0; u < 2; ++u) {
+        const int row = 32 * u + c32;
+        v4i kf[C::NKS];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s16[i] = (_Float16)((float)acc[i] * cs);
-          rml = (s16[i] > rml) ? s16[i] : rml;
-        }
-        const _Float16 rmo = (_Float16)xor32_f((float)rml);
-        const _Float16 rm = rml > rmo ? rml : rmo;
-        const _Float16 nm = m > rm ? m : rm;
-        const float r = exp2_f32((float)(_Float16)(m - nm));
-        m = nm;
-        float lt = 0.f;
-        float p32[16];
+        for (int s = 0; s < C::NKS; ++s)
+          kf[s] = *reinterpret_cast<const v4i*>(kl + row * D + 16 * ((2 * s + h) ^ k_sw<D>(row)));
+        acc[u] = mfma_i8(kf[0], qf[0], magic);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          p32[i] = exp2_f32((float)(_Float16)(s16[i] - nm));
-          lt += p32[i];
+        for (int s = 1; s < C::NKS; ++s) acc[u] = mfma_i8(kf[s], qf[s], acc[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u >= ntile) break;
+        // ---------------- softmax + per-row P quantisation (lane = query row), packed fp16
+        const float c = __uint_as_float(__float_as_uint(cq * (float)sk_lds[kb * 2 + u]) & ~3u);
+        const float cm = -12582912.0f * c;
+        v2h s2[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s2[j][0] = (_Float16)fmaf(__int_as_float(acc[u][2 * j]), c, cm);
+          s2[j][1] = (_Float16)fmaf(__int_as_float(acc[u][2 * j + 1]), c, cm);
         }
-        lt += xor32_f(lt);
+        v2h mx = __builtin_elementwise_max(__builtin_elementwise_max(s2[0], s2[1]),
+                                           __builtin_elementwise_max(s2[2], s2[3]));
+        mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(
+                                               __builtin_elementwise_max(s2[4], s2[5]),
+                                               __builtin_elementwise_max(s2[6], s2[7])));
+        const float rml = vmax((float)mx[0], (float)mx[1]);
+        const _Float16 rm = (_Float16)pair_max(rml);
+        // deferred max (cdna_hip_programming.md T13): keep the running max unless some row's tile
+        // max exceeds it by more than THR = 8 (log2 units); P_i8 depends only on S - rowmax and O, l
+        // share the stale reference, so O / l is unchanged up to rounding and operands stay <= 2^8.
+        const bool grow = __ballot((float)rm > (float)m + 8.0f) != 0;
+        float r = 1.0f;
+        if (grow) {
+          const _Float16 nm = m > rm ? m : rm;
+          r = exp2_f32((float)(_Float16)(m - nm));
+          m = nm;
+        }
+        const float er = exp2_f32((float)(_Float16)(rm - m));   // exp2(rm - m): P = e * er
+        const v2h rm2 = {rm, rm};
+        const _Float16 sp16 = (_Float16)(er * (1.0f / 127.0f));
+        const v2h sp2 = {sp16, sp16};
+        float esum = 0.f;
+        v4u pw[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          v2h d2[4], e2[4], t2[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d2[j] = s2[4 * g + j] - rm2;
+          exp2_pk4(d2, e2);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            esum = __builtin_amdgcn_fdot2(e2[j], one2, esum, false);
+            d2[j] = e2[j] * k127;
+          }
+          trunc_pk4(d2, t2);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pw[g][j] = __builtin_bit_cast(unsigned, t2[j] * sp2);
+        }
+        const float lt = pair_sum(esum) * er;
         l = l * r + lt;
-        const float e = exp2_f32((float)(_Float16)(rm - nm));
-        const float sp = e / 127.0f;
-        const float inv = 127.0f / e;
-        v8h pb[2];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float t = __builtin_truncf(p32[i] * inv);
-          pb[i >> 3][i & 7] = (_Float16)(t * sp);
-        }
-        // ---------------- rescale O (exact no-op when r == 1 for every row of the wave)
-        if (__ballot(r != 1.0f)) {
+        if (grow) {
 #pragma unroll
           for (int b = 0; b < C::NDB; ++b) o[b] *= r;
         }
@@ -196,21 +217,13 @@ __global__ __launch_bounds__(256, 2) void int8_attn_fwd_kernel(
             const int key_a = 32 * u + 16 * s + 4 * h + (i16 >> 2);
             const int ch = d / 8, within = (d % 8) * 2;
             const v8h a = __builtin_bit_cast(
-                v8h, ds_read_tr16_x2(vl + v_lds_off<D>(key_a, ch) + within,
-                                     vl + v_lds_off<D>(key_a + 8, ch) + within));
-            o[b] = mfma_f16(a, pb[s], o[b]);
-            if constexpr (DBG) {
-              if (blockIdx.x == 0 && wave == 0 && kb == 0 && u == 0 && b == 0 && s == 0) {
-                for (int i = 0; i < 16; ++i) dbg[lane * 16 + i] = (float)acc[i];
-                for (int i = 0; i < 16; ++i) dbg[1024 + lane * 16 + i] = (float)pb[i >> 3][i & 7];
-                for (int j = 0; j < 8; ++j) dbg[2048 + lane * 8 + j] = (float)a[j];
-              }
-            }
+                v8h, ds_read_tr16_x2(vl + key_a * 2 * D + 16 * (ch ^ v_sw<D>(key_a)) + within,
+                                     vl + (key_a + 8) * 2 * D + 16 * (ch ^ v_sw<D>(key_a + 8)) + within));
+            o[b] = mfma_f16(a, __builtin_bit_cast(v8h, pw[s]), o[b]);
           }
         }
       }
     }
-    if (kb + 1 < nkb) stage_store((kb + 1) & 1);
     __syncthreads();
   }
 
@@ -226,47 +239,35 @@ __global__ __launch_bounds__(256, 2) void int8_attn_fwd_kernel(
     for (int g = 0; g < 4; ++g) {
       v4h w;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = (_Float16)(o[b][4 * g + j] / l);
+      for (int j = 0; j < 4; ++j) w[j] = (_Float16)(o[b][4 * g + j] * il);
       *reinterpret_cast<v4h*>(orow + 32 * b + 8 * g + 4 * h) = w;
     }
   }
-  (void)il;
 }
 
 }  // namespace qattn
 
 using namespace qattn;
 
-extern "C" int qattn_probe_int8_attn_dbg(const void* q_i8, const void* sq, const void* k_i8,
-                                         const void* sk, const void* vdq, void* out, void* lse,
-                                         long bh, long seq, float qks, void* dbg, void* stream) {
-  const int nq = (int)((seq + 127) / 128);
-  hipLaunchKernelGGL((int8_attn_fwd_kernel<64, true>), dim3((unsigned)(nq * bh)), dim3(256),
-                     2 * Int8FwdCfg<64>::STAGE, (hipStream_t)stream, (const int8_t*)q_i8,
-                     (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
-                     (const _Float16*)vdq, (_Float16*)out, (_Float16*)lse, (int)bh, (int)seq, qks,
-                     (float*)dbg);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
 extern "C" int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
                                    const void* vdq, void* out, void* lse, long bh, long seq,
                                    int head_dim, float qks, void* stream) {
   if (seq % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
   if (bh == 0 || seq == 0) return 0;
-  const int nq = (int)((seq + 127) / 128);
-  dim3 grid((unsigned)(nq * bh)), block(256);
   hipStream_t st = (hipStream_t)stream;
-  if (head_dim == 128) {
-    hipLaunchKernelGGL((int8_attn_fwd_kernel<128>), grid, block, 2 * Int8FwdCfg<128>::STAGE, st,
-                       (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8,
-                       (const _Float16*)sk, (const _Float16*)vdq, (_Float16*)out, (_Float16*)lse,
-                       (int)bh, (int)seq, qks);
-  } else {
-    hipLaunchKernelGGL((int8_attn_fwd_kernel<64>), grid, block, 2 * Int8FwdCfg<64>::STAGE, st,
-                       (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8,
-                       (const _Float16*)sk, (const _Float16*)vdq, (_Float16*)out, (_Float16*)lse,
-                       (int)bh, (int)seq, qks);
+#define QA_LAUNCH(Dv)                                                                           \
+  {                                                                                             \
+    using C = Int8FwdCfg<Dv>;                                                                   \
+    const int nq = (int)((seq + C::QROWS - 1) / C::QROWS);                                      \
+    const int lds = 2 * C::STAGE + (int)(((seq / 32) * 2 + 15) / 16 * 16);                     \
+    hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<Dv>,                                  \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);                       \
+    hipLaunchKernelGGL((int8_attn_fwd_kernel<Dv>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds, st, \
+                       (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8,            \
+                       (const _Float16*)sk, (const _Float16*)vdq, (_Float16*)out, (_Float16*)lse, \
+                       (int)bh, (int)seq, qks);                                                 \
   }
+  if (head_dim == 128) QA_LAUNCH(128) else QA_LAUNCH(64)
+#undef QA_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

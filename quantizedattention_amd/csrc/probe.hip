@@ -63,3 +63,23 @@ extern "C" int qattn_probe_tr16(const void* M, void* out, void* stream) {
                      (const unsigned short*)M, (unsigned short*)out);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// packed-half helper probe: out[2i..2i+1] = {exp2_pk(x), trunc_pk(x*127)} per pair
+namespace qattn {
+__global__ void probe_pk_kernel(const v2h* x, v2h* e, v2h* t) {
+  const int i = threadIdx.x;   // 16 lanes x 4 pairs
+  if (i >= 16) return;
+  const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
+  v2h xi[4], xs[4], r[4];
+  for (int j = 0; j < 4; ++j) { xi[j] = x[4 * i + j]; xs[j] = xi[j] * k127; }
+  exp2_pk4(xi, r);
+  for (int j = 0; j < 4; ++j) e[4 * i + j] = r[j];
+  trunc_pk4(xs, r);
+  for (int j = 0; j < 4; ++j) t[4 * i + j] = r[j];
+}
+}  // namespace qattn
+extern "C" int qattn_probe_pk(const void* x, void* e, void* t, void* stream) {
+  hipLaunchKernelGGL(probe_pk_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const v2h*)x,
+                     (v2h*)e, (v2h*)t);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -42,3 +42,16 @@ def test_ds_read_tr16(lib):
         for q in range(4):
             exp[l, q] = M[4 * g + q, 16 * g + i]
     assert torch.equal(out.cpu(), exp)
+
+
+def test_packed_half_helpers(lib):
+    """exp2_pk / trunc_pk (e32 + SDWA WORD_1 pairs) equal per-element exp2 / trunc."""
+    from quantizedattention_amd import _lib
+    x = -torch.rand(128, generator=torch.Generator().manual_seed(3)).half() * 8
+    xd = x.cuda()
+    e = torch.empty_like(xd)
+    t = torch.empty_like(xd)
+    _lib.call("qattn_probe_pk", _lib.ptr(xd), _lib.ptr(e), _lib.ptr(t), _lib.stream_of(xd))
+    torch.cuda.synchronize()
+    assert torch.allclose(e.cpu().float(), torch.exp2(x.float()), rtol=2e-3, atol=0)
+    assert torch.equal(t.cpu().float(), torch.trunc((x * 127).float()))

@@ -1,0 +1,61 @@
+"""Launch one kernel of the int8 / bf16 paths N times at the headline shape (for rocprofv3 passes).
+
+    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd, int8_dkdv, int8_dq, bf16_fwd,
+                                                           bf16_bwd, jvp, quant
+"""
+import math
+import sys
+
+import torch
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from quantizedattention_amd import _lib  # noqa: E402
+from quantizedattention_amd.attention_int8 import _int8_forward, helion_atten_int8_hl_dot_bwd  # noqa: E402
+from quantizedattention_amd.attention_bf16 import (helion_atten_bf16_fwd_training,  # noqa: E402
+                                                   helion_flash_atten_2_algo_4_bwd)
+from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp32  # noqa: E402
+
+name = sys.argv[1]
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+B, H, S, D = 4, 32, 4096, 128
+g = torch.Generator(device="cuda").manual_seed(0)
+q, k, v = (torch.randn((B, H, S, D), device="cuda", generator=g).half() for _ in range(3))
+dO = (torch.randn((B, H, S, D), device="cuda", generator=g) * 1e-3).half()
+N = B * H * S
+P = _lib.ptr
+st = _lib.stream_of(q)
+qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
+sms = float(torch.tensor(1 / math.sqrt(D), dtype=torch.float32))
+O, lse, qi, kiT, vi, sq, sk, sv, km = _int8_forward(q, k, v, False)
+ki = kiT.t()
+vdq = torch.empty((N, D), dtype=torch.float16, device="cuda")
+_lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
+dOi = torch.empty((N, D), dtype=torch.int8, device="cuda")
+sdO = torch.empty((N // 32,), dtype=torch.float16, device="cuda")
+Dr = torch.empty((N,), dtype=torch.float32, device="cuda")
+_lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(dOi), P(sdO), P(Dr), B * H, S, D, st)
+dq, dk, dv = (torch.empty_like(q) for _ in range(3))
+vb = v.bfloat16()
+if name.startswith("bf16"):
+    Ob, lseb = helion_atten_bf16_fwd_training(q, k, vb, False)
+torch.cuda.synchronize()
+for _ in range(reps):
+    if name == "int8_fwd":
+        _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse), B * H, S, D, qks, st)
+    elif name == "int8_dkdv":
+        _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(lse),
+                  P(Dr), P(dk), P(dv), B * H, S, D, qks, sms, st)
+    elif name == "int8_dq":
+        _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(lse),
+                  P(Dr), P(dq), B * H, S, D, qks, sms, st)
+    elif name == "bf16_fwd":
+        helion_atten_bf16_fwd_training(q, k, vb, False)
+    elif name == "bf16_bwd":
+        helion_flash_atten_2_algo_4_bwd(q, k, vb, Ob, lseb, False, dO.float())
+    elif name == "jvp":
+        qq = q[:2, :16, :2048].contiguous().bfloat16()
+        helion_attention_jvp_forward_fp32(qq, qq, qq, qq, qq, qq)
+    elif name == "quant":
+        _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
+torch.cuda.synchronize()
+print("done", name, reps)
