@@ -128,8 +128,30 @@ QA_DEVICE void exp2_pk4(const v2h* x, v2h* r) { QA_PK4("v_exp_f16"); }
 QA_DEVICE void trunc_pk4(const v2h* x, v2h* r) { QA_PK4("v_trunc_f16"); }
 
 // LDS-DMA of one 16-B chunk per lane: the LDS destination is lds_base (wave-uniform) + 16*lane.
+// Issued from inline asm on purpose: hipcc cannot tell which LDS bytes a global_load_lds writes, so
+// for the builtin form it inserts s_waitcnt vmcnt(0) before every later ds_read (serialising the
+// prefetch of block j+1 with the compute of block j).  The asm form is invisible to its waitcnt
+// pass; the kernel waits for its own DMAs with dma_wait() before the barrier that publishes them.
 QA_DEVICE void glds16(const void* gsrc, void* lds_base) {
-  __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(lds_base));
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
+}
+// s_waitcnt vmcnt(0) as a real instruction hipcc's waitcnt pass understands: retire every ordinary
+// global load before a loop that issues asm LDS-DMA (otherwise the compiler's first-use wait for
+// those loads lands inside the loop and also waits for the in-flight DMA).
+QA_DEVICE void vmem_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// Wait for every outstanding VMEM op of this wave (incl. LDS-DMA) and LDS op, then barrier.
+QA_DEVICE void dma_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, cols 4p..4p+3 of a 4x16

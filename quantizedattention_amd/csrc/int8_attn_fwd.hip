@@ -23,10 +23,6 @@
 // sum_t sp*sv*(P_i8 . v_i8) (int8:249-250) runs inside the MFMA: exact up to the fp16 rounding of
 // the two dequantised operands (2^-12 relative each), and the D-wide per-tile i32->f32
 // dequantisation (8 VALU ops per score element) disappears.
-// The int8 accumulator starts at 0x4B400000 (C operand): its bit pattern is then the fp32 number
-// M + acc with M = 1.5 * 2^23 (exact while |acc| < 2^22; |acc| <= D*127^2), so
-// S = fma(bits, c, -M c) needs no i32->f32 convert.  c keeps 22 significant bits so that M*c = 3c*2^22
-// is exact and the fused multiply-add rounds acc*c once, straight to fp16 (v_fma_mix).
 #include "common.h"
 
 namespace qattn {
@@ -81,7 +77,10 @@ QA_DEVICE void stage_block(const int8_t* kbase, const _Float16* vbase, char* kl,
   }
 }
 
-template <int D>
+// AB (diagnostic timing builds only, never dispatched by the API): 1 = no softmax VALU,
+// 2 = no PV MFMA, 3 = no QK^T MFMA, 4 = no K/V streaming (LDS block 0 reused, no barriers),
+// 5 = 4 + no softmax.  Outputs of AB != 0 are meaningless.
+template <int D, int AB = 0>
 __global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
     const _Float16* __restrict__ sk, const _Float16* __restrict__ vdq, _Float16* __restrict__ out,
@@ -118,9 +117,6 @@ __global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
     sqw = (float)sq[(head_row0 + q0) / 32];
   }
   const float cq = sqw * qks;
-  v16i magic;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) magic[i] = 0x4B400000;
 
   v16f o[C::NDB];
 #pragma unroll
@@ -130,67 +126,108 @@ __global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
   const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
   const v2h one2 = {(_Float16)1.0f, (_Float16)1.0f};
 
+  // lane-constant LDS byte offsets (the swizzles depend only on row bits fixed per lane):
+  //   K A-operand chunk (2s+h) of row c32 (+32*D for the second tile)
+  //   V^T A-operand, d-block b: key rows 4h + (i16>>2) (+16 per k-step, +8 for the 2nd read,
+  //   +32 per tile), columns 32b + 16gg + 4(i16&3)
+  int koff[C::NKS], voff[C::NDB];
+#pragma unroll
+  for (int s = 0; s < C::NKS; ++s) koff[s] = c32 * D + 16 * ((2 * s + h) ^ k_sw<D>(c32));
+  {
+    const int gg = (lane >> 4) & 1, i16 = lane & 15;
+    const int key_a = 4 * h + (i16 >> 2);
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) {
+      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
+      voff[b] = key_a * 2 * D + 16 * ((d / 8) ^ v_sw<D>(key_a)) + (d % 8) * 2;
+    }
+  }
+
+  vmem_drain();
   __syncthreads();
+  dma_wait_barrier();
   for (int kb = 0; kb < nkb; ++kb) {
-    if (kb + 1 < nkb)
+    if (AB < 4 && kb + 1 < nkb)
       stage_block<D>(kbase, vbase, smem + ((kb + 1) & 1) * C::STAGE, (kb + 1) * C::KB, S, wave, lane);
-    const char* kl = smem + (kb & 1) * C::STAGE;
+    const char* kl = smem + (AB >= 4 ? 0 : (kb & 1)) * C::STAGE;
     const char* vl = kl + C::K_BYTES;
-    const int ntile = min(2, (S - kb * C::KB) / 32);
+    const bool two = (S - kb * C::KB) >= 64;   // the last block may hold a single 32-key tile
     if (active) {
-      // ---------------- S^T = K Q^T for both tiles first (independent int8 MFMA chains)
+      // ---------------- S^T = K Q^T for both tiles (independent int8 MFMA chains)
       v16i acc[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int row = 32 * u + c32;
         v4i kf[C::NKS];
 #pragma unroll
         for (int s = 0; s < C::NKS; ++s)
-          kf[s] = *reinterpret_cast<const v4i*>(kl + row * D + 16 * ((2 * s + h) ^ k_sw<D>(row)));
-        acc[u] = mfma_i8(kf[0], qf[0], magic);
+          kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s] + u * 32 * D);
+        if constexpr (AB == 3) {
 #pragma unroll
-        for (int s = 1; s < C::NKS; ++s) acc[u] = mfma_i8(kf[s], qf[s], acc[u]);
+          for (int i = 0; i < 16; ++i) acc[u][i] = kf[i & 3][i >> 2] + qf[i & 3][0];
+        } else {
+          acc[u] = mfma_i8(kf[0], qf[0], v16i{});
+#pragma unroll
+          for (int s = 1; s < C::NKS; ++s) acc[u] = mfma_i8(kf[s], qf[s], acc[u]);
+        }
       }
+      v4u pw[2][2];
+      if constexpr (AB == 1 || AB == 5) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pw[u][g][j] = (unsigned)acc[u][8 * g + 2 * j] & 0x3fff3fffu;
+      } else {
+      // ---------------- S = fp16(acc * sq*sk*qks), tile row maxima
+      v2h s2[2][8];
+      _Float16 rm[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        if (u >= ntile) break;
-        // ---------------- softmax + per-row P quantisation (lane = query row), packed fp16
-        const float c = __uint_as_float(__float_as_uint(cq * (float)sk_lds[kb * 2 + u]) & ~3u);
-        const float cm = -12582912.0f * c;
-        v2h s2[8];
+        const float c = cq * (float)sk_lds[min(kb * 2 + u, S / 32 - 1)];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          s2[j][0] = (_Float16)fmaf(__int_as_float(acc[u][2 * j]), c, cm);
-          s2[j][1] = (_Float16)fmaf(__int_as_float(acc[u][2 * j + 1]), c, cm);
+          s2[u][j][0] = (_Float16)((float)acc[u][2 * j] * c);
+          s2[u][j][1] = (_Float16)((float)acc[u][2 * j + 1] * c);
         }
-        v2h mx = __builtin_elementwise_max(__builtin_elementwise_max(s2[0], s2[1]),
-                                           __builtin_elementwise_max(s2[2], s2[3]));
+        v2h mx = __builtin_elementwise_max(__builtin_elementwise_max(s2[u][0], s2[u][1]),
+                                           __builtin_elementwise_max(s2[u][2], s2[u][3]));
         mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(
-                                               __builtin_elementwise_max(s2[4], s2[5]),
-                                               __builtin_elementwise_max(s2[6], s2[7])));
-        const float rml = vmax((float)mx[0], (float)mx[1]);
-        const _Float16 rm = (_Float16)pair_max(rml);
-        // deferred max (cdna_hip_programming.md T13): keep the running max unless some row's tile
-        // max exceeds it by more than THR = 8 (log2 units); P_i8 depends only on S - rowmax and O, l
-        // share the stale reference, so O / l is unchanged up to rounding and operands stay <= 2^8.
-        const bool grow = __ballot((float)rm > (float)m + 8.0f) != 0;
-        float r = 1.0f;
-        if (grow) {
-          const _Float16 nm = m > rm ? m : rm;
-          r = exp2_f32((float)(_Float16)(m - nm));
-          m = nm;
-        }
-        const float er = exp2_f32((float)(_Float16)(rm - m));   // exp2(rm - m): P = e * er
-        const v2h rm2 = {rm, rm};
+                                               __builtin_elementwise_max(s2[u][4], s2[u][5]),
+                                               __builtin_elementwise_max(s2[u][6], s2[u][7])));
+        rm[u] = (_Float16)pair_max(vmax((float)mx[0], (float)mx[1]));
+      }
+      if (!two) {  // a lone last tile: make tile 1 contribute exactly nothing
+        rm[1] = rm[0];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s2[1][j] = v2h{(_Float16)-65504.0f, (_Float16)-65504.0f};
+      }
+      // deferred max shared by the two tiles (cdna_hip_programming.md T13): the running max moves
+      // only when some row's tile max exceeds it by more than THR = 8 (log2 units).  P_i8 depends
+      // only on S - rowmax(tile); O and l share the (possibly stale) reference, so O / l is the
+      // same up to rounding, and the fp16 PV operands stay <= 2^8.
+      const _Float16 rmb = rm[0] > rm[1] ? rm[0] : rm[1];
+      const bool grow = __ballot((float)rmb > (float)m + 8.0f) != 0;
+      float r = 1.0f;
+      if (grow) {
+        const _Float16 nm = m > rmb ? m : rmb;
+        r = exp2_f32((float)(_Float16)(m - nm));
+        m = nm;
+      }
+      // ---------------- e = exp2(S - rm), P_i8 = trunc(127 e), operand = P_i8 * sp (packed fp16)
+      float lt = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float er = exp2_f32((float)(_Float16)(rm[u] - m));   // P = e * exp2(rm - m)
+        const v2h rm2 = {rm[u], rm[u]};
         const _Float16 sp16 = (_Float16)(er * (1.0f / 127.0f));
         const v2h sp2 = {sp16, sp16};
         float esum = 0.f;
-        v4u pw[2];
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
           v2h d2[4], e2[4], t2[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) d2[j] = s2[4 * g + j] - rm2;
+          for (int j = 0; j < 4; ++j) d2[j] = s2[u][4 * g + j] - rm2;
           exp2_pk4(d2, e2);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -199,32 +236,35 @@ __global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
           }
           trunc_pk4(d2, t2);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) pw[g][j] = __builtin_bit_cast(unsigned, t2[j] * sp2);
+          for (int j = 0; j < 4; ++j) pw[u][g][j] = __builtin_bit_cast(unsigned, t2[j] * sp2);
         }
-        const float lt = pair_sum(esum) * er;
-        l = l * r + lt;
-        if (grow) {
+        lt += esum * er;
+      }
+      l = l * r + pair_sum(lt);
+      if (grow) {
 #pragma unroll
-          for (int b = 0; b < C::NDB; ++b) o[b] *= r;
-        }
-        // ---------------- O^T += Vdq^T P^T (fp16 MFMA, fp32 accumulate)
+        for (int b = 0; b < C::NDB; ++b) o[b] *= r;
+      }
+      }
+      // ---------------- O^T += Vdq^T P^T (fp16 MFMA, fp32 accumulate)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
         for (int b = 0; b < C::NDB; ++b) {
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const int gg = (lane >> 4) & 1, i16 = lane & 15;
-            const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
-            const int key_a = 32 * u + 16 * s + 4 * h + (i16 >> 2);
-            const int ch = d / 8, within = (d % 8) * 2;
-            const v8h a = __builtin_bit_cast(
-                v8h, ds_read_tr16_x2(vl + key_a * 2 * D + 16 * (ch ^ v_sw<D>(key_a)) + within,
-                                     vl + (key_a + 8) * 2 * D + 16 * (ch ^ v_sw<D>(key_a + 8)) + within));
-            o[b] = mfma_f16(a, __builtin_bit_cast(v8h, pw[s]), o[b]);
+            const char* va = vl + voff[b] + (32 * u + 16 * s) * 2 * D;
+            const v8h a = __builtin_bit_cast(v8h, ds_read_tr16_x2(va, va + 8 * 2 * D));
+            if constexpr (AB == 2) {
+              asm volatile("" :: "v"(a), "v"(pw[u][s]));
+            } else {
+              o[b] = mfma_f16(a, __builtin_bit_cast(v8h, pw[u][s]), o[b]);
+            }
           }
         }
       }
     }
-    __syncthreads();
+    if constexpr (AB < 4) dma_wait_barrier();
   }
 
   if (!active) return;
@@ -269,5 +309,31 @@ extern "C" int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void*
   }
   if (head_dim == 128) QA_LAUNCH(128) else QA_LAUNCH(64)
 #undef QA_LAUNCH
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_int8_attn_fwd_ablate(const void* q_i8, const void* sq, const void* k_i8,
+                                          const void* sk, const void* vdq, void* out, void* lse,
+                                          long bh, long seq, float qks, int ab, void* stream) {
+  using C = Int8FwdCfg<128>;
+  const int nq = (int)((seq + C::QROWS - 1) / C::QROWS);
+  const int lds = 2 * C::STAGE + (int)(((seq / 32) * 2 + 15) / 16 * 16);
+  hipStream_t st = (hipStream_t)stream;
+#define QA_AB(A)                                                                                  \
+  hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<128, A>,                                  \
+                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);                           \
+  hipLaunchKernelGGL((int8_attn_fwd_kernel<128, A>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), \
+                     lds, st, (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8,       \
+                     (const _Float16*)sk, (const _Float16*)vdq, (_Float16*)out, (_Float16*)lse,    \
+                     (int)bh, (int)seq, qks);
+  switch (ab) {
+    case 1: QA_AB(1) break;
+    case 2: QA_AB(2) break;
+    case 3: QA_AB(3) break;
+    case 4: QA_AB(4) break;
+    case 5: QA_AB(5) break;
+    default: QA_AB(0) break;
+  }
+#undef QA_AB
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -43,9 +43,7 @@ QA_DEVICE void dma_tile(const char* gsrc, char* lds_tile, int wave, int lane) {
     const int row = inst * RPI + lane / C::NCH;
     const int p = lane % C::NCH;
     const int ch = p ^ (TR ? jtr_sw<D>(row) : jrow_sw<D>(row));
-    __builtin_amdgcn_global_load_lds(
-        reinterpret_cast<const void*>(gsrc + (long)row * C::ROWB + 16 * ch),
-        (__attribute__((address_space(3))) void*)(lds_tile + inst * 1024), 16, 0, 0);
+    glds16(gsrc + (long)row * C::ROWB + 16 * ch, lds_tile + inst * 1024);
   }
 }
 
@@ -105,7 +103,8 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(
     dma_tile<D, true>(gtv + off, base + 3 * C::TILE, wave, lane);
   };
   stage(0, 0);
-  __syncthreads();
+  vmem_drain();
+  dma_wait_barrier();
   for (int kb = 0; kb < nkb; ++kb) {
     if (kb + 1 < nkb) stage(kb + 1, (kb + 1) & 1);
     const char* base = smem + (kb & 1) * C::STAGE;
@@ -174,7 +173,7 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(
         }
       }
     }
-    __syncthreads();
+    dma_wait_barrier();
   }
   if (!active) return;
   const long r = (long)bh * Sq + qi;
