@@ -106,7 +106,8 @@ def int8_kernel_times(q, k, v, dO, n):
     km = e(B * H, D, dt=torch.float16)
     O = e(B, H, S, D, dt=torch.float16)
     lse = e(N, dt=torch.float16)
-    Dr = e(N, dt=torch.float32)
+    LD = e(N, 2, dt=torch.float32)
+    qb, kb, ob = (e(N, D, dt=torch.bfloat16) for _ in range(3))
     dq, dk, dv = (e(B, H, S, D, dt=torch.float16) for _ in range(3))
     qks, sms = _f32(1 / math.sqrt(D) * 1.44269504), _f32(1 / math.sqrt(D))
     calls = {
@@ -119,13 +120,18 @@ def int8_kernel_times(q, k, v, dO, n):
                                                      None, N, S, D, st),
         "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk),
                                                   P(vdq), P(O), P(lse), B * H, S, D, qks, st),
-        "int8_bwd_prep": lambda: _lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(dOi), P(sdO), P(Dr),
-                                           B * H, S, D, st),
-        "int8_bwd_dkdv_kernel": lambda: _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi), P(sq),
-                                                  P(ki), P(sk), P(vi), P(sv), P(lse), P(Dr), P(dk),
-                                                  P(dv), B * H, S, D, qks, sms, st),
+        "int8_bwd_prep": lambda: _lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(lse), P(dOi), P(sdO),
+                                           P(LD), B * H, S, D, st),
+        "i8_to_bf16_kernel(x3)": lambda: [_lib.call("qattn_i8_to_bf16", P(a), P(b), N * D, st)
+                                          for a, b in ((qi, qb), (ki, kb), (dOi, ob))],
+        "int8_bwd_dkdv_kernel<dV>": lambda: _lib.call("qattn_int8_bwd_dv", P(dOi), P(sdO), P(qi), P(sq),
+                                                  P(ki), P(sk), P(vi), P(sv), P(LD), P(qb), P(ob),
+                                                  P(dk), P(dv), B * H, S, D, qks, sms, st),
+        "int8_bwd_dkdv_kernel<dK>": lambda: _lib.call("qattn_int8_bwd_dk", P(dOi), P(sdO), P(qi), P(sq),
+                                                  P(ki), P(sk), P(vi), P(sv), P(LD), P(qb), P(ob),
+                                                  P(dk), P(dv), B * H, S, D, qks, sms, st),
         "int8_bwd_dq_kernel": lambda: _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq),
-                                                P(ki), P(sk), P(vi), P(sv), P(lse), P(Dr), P(dq),
+                                                P(ki), P(sk), P(vi), P(sv), P(LD), P(kb), P(dq),
                                                 B * H, S, D, qks, sms, st),
     }
     order = list(calls)
@@ -216,12 +222,13 @@ def main():
     kt = int8_kernel_times(q, k, v, dO, max(3, a.steps // 2))
     per_call = {  # algorithmic MFMA work per launch
         "int8_attn_fwd_kernel": 4.0 * B * H * S * S * D,   # QK^T, PV
-        "int8_bwd_dkdv_kernel": 8.0 * B * H * S * S * D,   # S, dP, dV, dK
+        "int8_bwd_dkdv_kernel<dV>": 4.0 * B * H * S * S * D,   # S, dV
+        "int8_bwd_dkdv_kernel<dK>": 6.0 * B * H * S * S * D,   # S, dP, dK
         "int8_bwd_dq_kernel": 6.0 * B * H * S * S * D,     # S, dP (recomputed), dQ
     }
     dom = max(per_call, key=lambda n: kt[n])
     achieved = per_call[dom] / (kt[dom] * 1e-3) / 1e12
-    fwd_ms = sum(v for n, v in kt.items() if not n.startswith("int8_bwd"))
+    fwd_ms = sum(v for n, v in kt.items() if not n.startswith(("int8_bwd", "i8_to_bf16")))
     out = {
         "metric": "fused-attn fwd+bwd TFLOP/s & us/call at (B,H,S,D)=(4,32,4096,128), int8 vs bf16",
         "value": world * flop_fb / t_i8 / 1e12,

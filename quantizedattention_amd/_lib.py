@@ -25,9 +25,12 @@ SIGNATURES = {
     "qattn_int8_quant": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_int, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_int8_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _c_float, _vp],
-    "qattn_int8_bwd_prep": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
-    "qattn_int8_attn_bwd": [_vp] * 16 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
-    "qattn_int8_bwd_dkdv": [_vp] * 12 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
+    "qattn_int8_bwd_prep": [_vp] * 6 + [_c_long, _c_long, _c_int, _vp],
+    "qattn_i8_to_bf16": [_vp, _vp, _c_long, _vp],
+    "qattn_int8_attn_bwd": [_vp] * 15 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
+    "qattn_int8_bwd_dkdv": [_vp] * 13 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
+    "qattn_int8_bwd_dv": [_vp] * 13 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
+    "qattn_int8_bwd_dk": [_vp] * 13 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_int8_bwd_dq": [_vp] * 11 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_bf16_fwd": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
     "qattn_bf16_bwd_prep": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],

@@ -131,9 +131,16 @@ def helion_atten_int8_hl_dot_bwd(
     v_i8 = v_bh_int8.contiguous()
     dO_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
     sdO = torch.empty((N // BQ,), dtype=torch.float16, device=dev)
-    Drow = torch.empty((N,), dtype=torch.float32, device=dev)
-    _lib.call("qattn_int8_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(dO_i8), _lib.ptr(sdO),
-              _lib.ptr(Drow), B * H, S, D, st)
+    LD = torch.empty((N, 2), dtype=torch.float32, device=dev)  # {lse, D} per row
+    lse = lse_input_fp16.to(torch.float16).contiguous()
+    _lib.call("qattn_int8_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(lse), _lib.ptr(dO_i8),
+              _lib.ptr(sdO), _lib.ptr(LD), B * H, S, D, st)
+    # exact bf16 copies of the int8 operands read column-wise by the accumulating products
+    q_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
+    k_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
+    dO_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
+    for src, dst in ((q_i8, q_bf), (k_i8, k_bf), (dO_i8, dO_bf)):
+        _lib.call("qattn_i8_to_bf16", _lib.ptr(src), _lib.ptr(dst), N * D, st)
     dq = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
     dk = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
     dv = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
@@ -141,8 +148,8 @@ def helion_atten_int8_hl_dot_bwd(
     sms = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
     _lib.call("qattn_int8_attn_bwd", _lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8),
               _lib.ptr(sq_bh_fp16.contiguous()), _lib.ptr(k_i8), _lib.ptr(sk_bh_fp16.contiguous()),
-              _lib.ptr(v_i8), _lib.ptr(sv_bh_fp16.contiguous()), _lib.ptr(lse_input_fp16.contiguous()),
-              _lib.ptr(Drow), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), None, None, None,
+              _lib.ptr(v_i8), _lib.ptr(sv_bh_fp16.contiguous()), _lib.ptr(LD), _lib.ptr(q_bf),
+              _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
               B * H, S, D, qks, sms, st)
     return dq, dk, dv
 

@@ -32,8 +32,11 @@ vdq = torch.empty((N, D), dtype=torch.float16, device="cuda")
 _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 dOi = torch.empty((N, D), dtype=torch.int8, device="cuda")
 sdO = torch.empty((N // 32,), dtype=torch.float16, device="cuda")
-Dr = torch.empty((N,), dtype=torch.float32, device="cuda")
-_lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(dOi), P(sdO), P(Dr), B * H, S, D, st)
+LD = torch.empty((N, 2), dtype=torch.float32, device="cuda")
+_lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(lse), P(dOi), P(sdO), P(LD), B * H, S, D, st)
+qb, kb, ob = (torch.empty((N, D), dtype=torch.bfloat16, device="cuda") for _ in range(3))
+for a_, b_ in ((qi, qb), (ki, kb), (dOi, ob)):
+    _lib.call("qattn_i8_to_bf16", P(a_), P(b_), N * D, st)
 dq, dk, dv = (torch.empty_like(q) for _ in range(3))
 vb = v.bfloat16()
 if name.startswith("bf16"):
@@ -43,11 +46,11 @@ for _ in range(reps):
     if name == "int8_fwd":
         _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse), B * H, S, D, qks, st)
     elif name == "int8_dkdv":
-        _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(lse),
-                  P(Dr), P(dk), P(dv), B * H, S, D, qks, sms, st)
+        _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
+                  P(qb), P(ob), P(dk), P(dv), B * H, S, D, qks, sms, st)
     elif name == "int8_dq":
-        _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(lse),
-                  P(Dr), P(dq), B * H, S, D, qks, sms, st)
+        _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
+                  P(kb), P(dq), B * H, S, D, qks, sms, st)
     elif name == "bf16_fwd":
         helion_atten_bf16_fwd_training(q, k, vb, False)
     elif name == "bf16_bwd":
