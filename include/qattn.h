@@ -1,0 +1,146 @@
+/*
+ * qattn.h — C ABI of libqattn.so, the MI355X (gfx950) hot path of selau642/QuantizedAttention.
+ *
+ * The reference (three Python modules over Helion/Triton kernels) has no native boundary of its
+ * own: each entry point below replaces one @helion.kernel call (or the torch glue around it) and is
+ * cited as reference `file:line`.  The Python mirror of the reference's public functions
+ * (quantizedattention_amd/attention_{int8,bf16,jvp}.py) binds exactly these symbols through ctypes
+ * (quantizedattention_amd/_lib.py); INTEGRATION.md shows the binding for other hosts.
+ *
+ * Conventions (all entries):
+ *   - Plain device pointers (HBM, allocated by the caller, contiguous row-major), sizes as long/int,
+ *     `stream` is a hipStream_t (NULL = the default stream).  Work is enqueued asynchronously on
+ *     `stream`; nothing is synchronised and no memory is allocated by the library.
+ *   - Return value: 0 = enqueued, 1 = unsupported shape / argument (nothing launched),
+ *     2 = launch failure (hipGetLastError() != hipSuccess).
+ *   - "rows" N = BH * S with BH = batch * heads; tensors [B,H,S,D] are addressed as [BH*S, D].
+ *     Block-scale arrays hold one fp16 per 32 consecutive rows: index (b*H+h)*S/32 + s/32
+ *     (attention_int8.py:161-168).
+ *   - qks = fp32(1/sqrt(D) * 1.44269504) (attention_int8.py:151-153, attention_bf16.py:188-190);
+ *     sms = fp32(1/sqrt(D)).  lse values are base-2 (log2 of the softmax denominator plus max).
+ *   - head_dim D in {64, 128}.  Dtypes: i8 = int8_t, f16 = _Float16 (IEEE half), bf16 = bfloat16,
+ *     f32 = float.
+ */
+#ifndef QATTN_H
+#define QATTN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- int8 path (attention_int8.py) */
+
+/* Per-32-row block quantiser (attention_int8.py:178-186 q, 188-195 k, 241-247 v).
+ *   x      f16 [rows, D]              in
+ *   idx    i8  [rows, D]              out: trunc(RNE_f16(f32(x') / f32(s)))
+ *   scale  f16 [rows/32]              out: s = RNE_f16(amax|x'| / 127)   (all-zero block: s = 0, idx 0)
+ *   deq    f16 [rows, D] or NULL      out: f16(idx * s)  (the fp16 operand of the forward P.V product)
+ *   kmean  f16 [rows/rows_per_head, D] or NULL: when given, x' = f16(x - kmean[head]) (k-smoothing,
+ *          build contract for attention_int8.py:24-25), else x' = x.
+ * Bit-exact with the reference's eager-torch rounding.  rows % 32 == 0. */
+int qattn_int8_quant(const void* x, void* idx, void* scale, void* deq, const void* kmean, long rows,
+                     int rows_per_head, int head_dim, void* stream);
+
+/* k_mean = f16(mean over the S tokens of each head) — k f16 [bh*seq, D] -> kmean f16 [bh, D]
+ * (SageAttention smoothing; replaces the crashing `k.mean(0)` of attention_int8.py:24-25). */
+int qattn_kmean(const void* k, void* kmean, long bh, long seq, int head_dim, void* stream);
+
+/* int8 SageAttention-3 forward, per (batch, head) (attention_int8.py:197-257; per-head contract F2).
+ *   q_i8, k_i8  i8 [bh*seq, D]; sq, sk f16 [bh*seq/32]; vdq f16 [bh*seq, D] (= qattn_int8_quant deq
+ *   of v); out O f16 [bh*seq, D]; lse f16 [bh*seq] (base 2).  S = f16(f32(q_i8.k_i8) * sq*sk*qks),
+ *   P = exp2(S - m), P.V on int8-quantised P (sp = exp2(rowmax - m)/127).  seq % 32 == 0. */
+int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
+                        const void* vdq, void* out, void* lse, long bh, long seq, int head_dim,
+                        float qks, void* stream);
+
+/* Backward prologue (attention_int8.py:372-374, 398): dO f16 -> dO_i8 [rows, D] + sdO f16 [rows/32]
+ * (same quantiser), and LD f32x2 [rows] = {f32(lse), f32(f16(rowsum(dO*O)))}. */
+int qattn_int8_bwd_prep(const void* dO, const void* O, const void* lse, void* dO_i8, void* sdO,
+                        void* LD, long bh, long seq, int head_dim, void* stream);
+
+/* Exact widening copy i8 -> bf16 of n elements (n % 16 == 0): the transposed-read operand images
+ * of q_i8, k_i8, dO_i8 used by the dK / dQ / dV products (no reference counterpart). */
+int qattn_i8_to_bf16(const void* x, void* y, long n, void* stream);
+
+/* Corrected int8 backward (attention_int8.py:268-432 with SURVEY F4 fixed: dS = P*(dP - D),
+ * sm_scale, deterministic per-head accumulation, k_mean term dropped since rowsum(dS) = 0).
+ * Quantisation granularity as the reference: P and dS per 32x32 tile (amax/127, trunc), dO per
+ * 32-row block, q/k/v int8 + scales from the forward.  Launches the dV, dK and dQ kernels.
+ *   dq, dk, dv f16 [bh*seq, D] out; q_bf/k_bf/dO_bf = qattn_i8_to_bf16 images. */
+int qattn_int8_attn_bwd(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                        const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                        const void* LD, const void* q_bf, const void* k_bf, const void* dO_bf,
+                        void* dq, void* dk, void* dv, long bh, long seq, int head_dim, float qks,
+                        float sms, void* stream);
+
+/* The parts of qattn_int8_attn_bwd, launchable alone (per-kernel timing / overlap):
+ * dK and dV (attention_int8.py:375-378, 423-428), dV only, dK only, dQ only (414-420). */
+int qattn_int8_bwd_dkdv(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                        const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                        const void* LD, const void* q_bf, const void* dO_bf, void* dk, void* dv,
+                        long bh, long seq, int head_dim, float qks, float sms, void* stream);
+int qattn_int8_bwd_dv(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                      const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                      const void* LD, const void* q_bf, const void* dO_bf, void* dk, void* dv,
+                      long bh, long seq, int head_dim, float qks, float sms, void* stream);
+int qattn_int8_bwd_dk(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                      const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                      const void* LD, const void* q_bf, const void* dO_bf, void* dk, void* dv,
+                      long bh, long seq, int head_dim, float qks, float sms, void* stream);
+int qattn_int8_bwd_dq(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                      const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                      const void* LD, const void* k_bf, void* dq, long bh, long seq, int head_dim,
+                      float qks, float sms, void* stream);
+
+/* ---------------------------------------------------------------- bf16 path (attention_bf16.py) */
+
+/* FA2 forward with the reference's "multiple-max" beta rule emulated per 16-key sub-tile
+ * (helion_atten_bf16_fwd_training, attention_bf16.py:107-296).
+ *   q, k f16 [bh*sq|sk, D]; v bf16 [bh*sk, D]; out O f32 [bh*sq, D]; lse f32 [bh*sq] (base 2).
+ *   causal: strict-lower mask with fill -126 in raw logit units (attention_bf16.py:222-233).
+ *   sq % 32 == 0, sk % 32 == 0. */
+int qattn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
+                   long sq, long sk, int head_dim, int causal, float qks, void* stream);
+
+/* Backward prologue: dO f32 -> dO_bf bf16 [rows, D] and Drow f32 [rows] = rowsum(dO*O)
+ * (attention_bf16.py:416, computed once per row instead of per tile). */
+int qattn_bf16_bwd_prep(const void* dO, const void* O, void* dO_bf, void* Drow, long bh, long seq,
+                        int head_dim, void* stream);
+
+/* Corrected FA2 backward (helion_flash_atten_2_algo_4_bwd, attention_bf16.py:299-448 with SURVEY F3
+ * fixed: dS = P*(dP - D), sm_scale, deterministic dq).  q, k f16; v bf16; dO_bf bf16; lse, Drow f32;
+ * out dq [bh*sq, D], dk, dv [bh*sk, D] f32.  sq % 32 == 0, sk % 64 == 0. */
+int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf, const void* lse,
+                   const void* Drow, void* dq, void* dk, void* dv, long bh, long sq, long sk,
+                   int head_dim, int causal, float qks, float sms, void* stream);
+
+/* ---------------------------------------------------------------- JVP (attention_jvp.py) */
+
+/* Forward-mode tangent attention (helion_attention_jvp_forward_fp32, attention_jvp.py:24-195):
+ *   q, k, v, tq, tk, tv bf16 [bh*sq|sk, D]; out O, tO f32 [bh*sq, D]; lse f32 [bh*sq] (base 2).
+ *   tO = (P.tV + (P o tS).V - rowsum(P o tS) * O) / l with tS = (tq.k^T + q.tk^T) * sm.
+ *   flags must be 0 (reserved).  sq % 32 == 0, sk % 64 == 0. */
+int qattn_jvp_fwd(const void* q, const void* k, const void* v, const void* tq, const void* tk,
+                  const void* tv, void* out, void* tout, void* lse, long bh, long sq, long sk,
+                  int head_dim, int flags, float qks, float sm, void* stream);
+
+/* ---------------------------------------------------------------- diagnostics (not product API) */
+
+/* qattn_int8_attn_fwd with parts of the tile pipeline disabled (ab = 0 full, 1 no softmax,
+ * 2 no P.V, 3 no QK^T, 4 no K/V streaming, 5 = 1+4); D = 128 only.  Output is NOT attention for
+ * ab != 0: used by tools/ablate.py to attribute kernel time. */
+int qattn_int8_attn_fwd_ablate(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
+                               const void* vdq, void* out, void* lse, long bh, long seq, float qks,
+                               int ab, void* stream);
+
+/* MFMA / LDS-transpose fragment-layout probes (one wave; tests/test_gpu_layout.py). */
+int qattn_probe_mfma_i8(const void* A, const void* B, void* C, void* stream);
+int qattn_probe_mfma_f16(const void* A, const void* B, void* C, void* stream);
+int qattn_probe_tr16(const void* M, void* out, void* stream);
+int qattn_probe_pk(const void* x, void* e, void* t, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QATTN_H */

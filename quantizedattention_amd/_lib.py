@@ -33,8 +33,8 @@ SIGNATURES = {
     "qattn_int8_bwd_dk": [_vp] * 13 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_int8_bwd_dq": [_vp] * 11 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_bf16_fwd": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
-    "qattn_bf16_bwd_prep": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
-    "qattn_bf16_bwd": [_vp] * 12 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
+    "qattn_bf16_bwd_prep": [_vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
+    "qattn_bf16_bwd": [_vp] * 9 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
     "qattn_jvp_fwd": [_vp] * 9 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
     "qattn_int8_attn_fwd_ablate": [_vp] * 7 + [_c_long, _c_long, _c_float, _c_int, _vp],
     "qattn_probe_mfma_i8": [_vp, _vp, _vp, _vp],
@@ -64,7 +64,7 @@ def load(path: os.PathLike | None = None) -> ctypes.CDLL:
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name, None)
         if fn is None:
-            continue
+            raise QAttnError(f"{p} does not export {name} (stale build? rebuild it)")
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
     _lib = lib

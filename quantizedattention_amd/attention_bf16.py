@@ -96,7 +96,7 @@ def helion_flash_atten_2_algo_4_bwd(
     st = _lib.stream_of(q)
     dO_bf = torch.empty((B, H, S, D), dtype=torch.bfloat16, device=dev)
     Drow = torch.empty((B * H, S), dtype=torch.float32, device=dev)
-    _lib.call("qattn_bf16_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(dO_bf), _lib.ptr(Drow), None,
+    _lib.call("qattn_bf16_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(dO_bf), _lib.ptr(Drow),
               B * H, S, D, st)
     dq = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
     dk = torch.empty((B, H, Sk, D), dtype=torch.float32, device=dev)
@@ -104,7 +104,7 @@ def helion_flash_atten_2_algo_4_bwd(
     qks = _f32(1.0 / math.sqrt(D) * 1.44269504)
     sms = _f32(1.0 / math.sqrt(D))
     _lib.call("qattn_bf16_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(lse),
-              _lib.ptr(Drow), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), None, None, None,
+              _lib.ptr(Drow), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
               B * H, S, Sk, D, int(bool(causal)), qks, sms, st)
     return dq, dk, dv
 

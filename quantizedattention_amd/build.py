@@ -13,6 +13,7 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
+INCLUDE = PKG.parent / "include"
 BUILD = PKG / "_build"
 LIB = PKG / "libqattn.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -20,7 +21,7 @@ ARCH = "gfx950"
 CFLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
     "-fhip-fp32-correctly-rounded-divide-sqrt",  # the quantiser needs IEEE fp32 division
-    "-fno-gpu-rdc", "-Wno-unused-result",
+    "-fno-gpu-rdc", "-Wno-unused-result", f"-I{INCLUDE}",
 ]
 
 
@@ -34,7 +35,7 @@ def _compile(src: Path, obj: Path) -> str:
 
 def build(verbose: bool = True, jobs: int = 8) -> Path:
     BUILD.mkdir(exist_ok=True)
-    headers = list(CSRC.glob("*.h"))
+    headers = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
     hdr_mtime = max((h.stat().st_mtime for h in headers), default=0.0)
     srcs = sorted(CSRC.glob("*.hip"))
     todo = []

@@ -406,9 +406,8 @@ static void set_lds(K kernel, int bytes) {
 
 using namespace qattn;
 
-extern "C" int qattn_bf16_bwd_prep(const void* dO, const void* O, void* dO_bf, void* Drow,
-                                   void* unused, long bh, long seq, int head_dim, void* stream) {
-  (void)unused;
+extern "C" int qattn_bf16_bwd_prep(const void* dO, const void* O, void* dO_bf, void* Drow, long bh,
+                                   long seq, int head_dim, void* stream) {
   if (head_dim != 64 && head_dim != 128) return 1;
   const long rows = bh * seq;
   if (rows == 0) return 0;
@@ -426,9 +425,8 @@ extern "C" int qattn_bf16_bwd_prep(const void* dO, const void* O, void* dO_bf, v
 
 extern "C" int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf,
                               const void* lse, const void* Drow, void* dq, void* dk, void* dv,
-                              void* ws0, void* ws1, void* ws2, long bh, long sq, long sk,
-                              int head_dim, int causal, float qks, float sms, void* stream) {
-  (void)ws0; (void)ws1; (void)ws2;
+                              long bh, long sq, long sk, int head_dim, int causal, float qks,
+                              float sms, void* stream) {
   if (sq % 32 != 0 || sk % 64 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
   if (bh == 0 || sq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "qattn.h"  // the C ABI: every extern "C" definition is checked against its declaration
+
 namespace qattn {
 
 typedef int v4i __attribute__((ext_vector_type(4)));

@@ -202,8 +202,7 @@ using namespace qattn;
 extern "C" int qattn_jvp_fwd(const void* q, const void* k, const void* v, const void* tq, const void* tk,
                              const void* tv, void* out, void* tout, void* lse, long bh, long sq, long sk,
                              int head_dim, int flags, float qks, float sm, void* stream) {
-  (void)flags;
-  if (sq % 32 != 0 || sk % 64 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  if (flags != 0 || sq % 32 != 0 || sk % 64 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
   if (bh == 0 || sq == 0) return 0;
   const int nq = (int)((sq + 127) / 128);
   hipStream_t st = (hipStream_t)stream;
