@@ -1,6 +1,6 @@
 """Launch one kernel of the int8 / bf16 paths N times at the headline shape (for rocprofv3 passes).
 
-    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd, int8_dkdv, int8_dq, bf16_fwd,
+    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd, int8_dkdv, int8_dv, int8_dk, int8_dq, int8_all, bf16_fwd,
                                                            bf16_bwd, jvp, quant
 """
 import math
@@ -16,6 +16,10 @@ from quantizedattention_amd.attention_bf16 import (helion_atten_bf16_fwd_trainin
 from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp32  # noqa: E402
 
 name = sys.argv[1]
+if name == "int8_all":  # every int8 attention kernel once per rep, in step order
+    names = ["int8_fwd", "int8_dv", "int8_dk", "int8_dq"]
+else:
+    names = [name]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 B, H, S, D = 4, 32, 4096, 128
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -42,12 +46,15 @@ vb = v.bfloat16()
 if name.startswith("bf16"):
     Ob, lseb = helion_atten_bf16_fwd_training(q, k, vb, False)
 torch.cuda.synchronize()
-for _ in range(reps):
+for name in [n for _ in range(reps) for n in names]:
     if name == "int8_fwd":
         _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse), B * H, S, D, qks, st)
     elif name == "int8_dkdv":
         _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
                   P(qb), P(ob), P(dk), P(dv), B * H, S, D, qks, sms, st)
+    elif name in ("int8_dv", "int8_dk"):
+        _lib.call("qattn_" + name.replace("int8_", "int8_bwd_"), P(dOi), P(sdO), P(qi), P(sq), P(ki),
+                  P(sk), P(vi), P(sv), P(LD), P(qb), P(ob), P(dk), P(dv), B * H, S, D, qks, sms, st)
     elif name == "int8_dq":
         _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
                   P(kb), P(dq), B * H, S, D, qks, sms, st)
@@ -61,4 +68,4 @@ for _ in range(reps):
     elif name == "quant":
         _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 torch.cuda.synchronize()
-print("done", name, reps)
+print("done", sys.argv[1], reps)

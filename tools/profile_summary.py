@@ -1,0 +1,109 @@
+"""Turn a tools/profile_round.sh output directory into the committed profile artefacts.
+
+    python tools/profile_summary.py gpurun_out/prof_<tag> <tag>
+
+Writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats of the bench command (verbatim)
+  profiles/<tag>_bench.json         the bench JSON line printed under the profiler
+  profiles/<tag>_pmc.json           per kernel: FETCH_SIZE (raw and x2-corrected), WRITE_SIZE, MFMA busy
+  profiles/traffic_latest.json      bench kernel key -> HBM bytes per launch (FETCH x2 + WRITE), which
+                                    bench.py reports as roofline.traffic
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "profiles")
+
+# bench.py kernel keys -> normalised rocprof kernel-name patterns (D = 128 instantiations)
+KEYS = {
+    "int8_attn_fwd_kernel": r"int8_attn_fwd_kernel(<128(,0)?>|ILi128ELi0E|ILi128EE)",
+    "int8_bwd_dkdv_kernel<dV>": r"int8_bwd_dkdv_kernel(<128,1>|ILi128ELi1E)",
+    "int8_bwd_dkdv_kernel<dK>": r"int8_bwd_dkdv_kernel(<128,2>|ILi128ELi2E)",
+    "int8_bwd_dq_kernel": r"int8_bwd_dq_kernel(<128>|ILi128E)",
+}
+SIMDS_PER_XCD = 32 * 4
+# GRBM_GUI_ACTIVE is summed over the 8 XCDs; SQ_VALU_MFMA_BUSY_CYCLES counts 32 busy SIMD-cycles per
+# 32x32 MFMA (i8 32x32x32 and f16/bf16 32x32x16 alike: 65536 / 32768 ops at 2048 / 1024 ops/clk/SIMD)
+XCDS = 8
+
+
+def norm(name):
+    return re.sub(r"\s+", "", name)
+
+
+def key_of(name):
+    n = norm(name)
+    for k, pat in KEYS.items():
+        if re.search(pat, n):
+            return k
+    return None
+
+
+def counters(d):
+    """{bench key: {counter: mean per dispatch}} from one --pmc pass directory."""
+    per = defaultdict(float)
+    kinds = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            k = key_of(row["Kernel_Name"])
+            if k is None:
+                continue
+            per[(k, row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
+            kinds[k] = True
+    acc = defaultdict(lambda: defaultdict(list))
+    for (k, _, c), v in per.items():
+        acc[k][c].append(v)
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    os.makedirs(PROF, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "bench", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    bj = os.path.join(src, "bench.json")
+    if os.path.exists(bj):
+        lines = [ln for ln in open(bj) if ln.startswith("{")]
+        if lines:
+            with open(os.path.join(PROF, f"{tag}_bench.json"), "w") as f:
+                f.write(lines[-1])
+    fetch = counters(os.path.join(src, "fetch"))
+    write = counters(os.path.join(src, "write"))
+    mfma = counters(os.path.join(src, "mfma"))
+    out, traffic = {}, {}
+    for k in KEYS:
+        e = {}
+        if k in fetch:
+            e["FETCH_SIZE_raw_bytes"] = fetch[k]["FETCH_SIZE"] * 1024
+            e["FETCH_bytes_x2"] = 2 * e["FETCH_SIZE_raw_bytes"]
+        if k in write:
+            e["WRITE_bytes"] = write[k]["WRITE_SIZE"] * 1024
+        if k in mfma and mfma[k].get("GRBM_GUI_ACTIVE"):
+            m = mfma[k]
+            e.update(m)
+            cyc = m["GRBM_GUI_ACTIVE"] / XCDS
+            e["mfma_util"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS_PER_XCD * XCDS)
+            e["gpu_cycles"] = cyc
+        if "FETCH_bytes_x2" in e and "WRITE_bytes" in e:
+            traffic[k] = e["FETCH_bytes_x2"] + e["WRITE_bytes"]
+            e["hbm_bytes_per_launch"] = traffic[k]
+        out[k] = e
+    with open(os.path.join(PROF, f"{tag}_pmc.json"), "w") as f:
+        json.dump({"note": "FETCH_SIZE/WRITE_SIZE are KB per dispatch from rocprofv3; FETCH doubled "
+                           "per MI355X_MICROARCH.md (gfx950 reports half of wide streaming reads)",
+                   "kernels": out}, f, indent=1)
+    with open(os.path.join(PROF, "traffic_latest.json"), "w") as f:
+        json.dump(traffic, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
