@@ -138,6 +138,10 @@ int qattn_probe_mfma_i8(const void* A, const void* B, void* C, void* stream);
 int qattn_probe_mfma_f16(const void* A, const void* B, void* C, void* stream);
 int qattn_probe_tr16(const void* M, void* out, void* stream);
 int qattn_probe_pk(const void* x, void* e, void* t, void* stream);
+/* int8-forward softmax helpers on 16 lanes: w = f16(trunc(127 e) * sp) via the round-toward-zero
+ * packed fma; d = {f16(a*c + n)} via v_fma_mix (cn holds (c, n) per lane). */
+int qattn_probe_fwd_helpers(const void* e, const void* sp, void* w, const void* a, const void* cn,
+                            void* d, void* stream);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,7 @@ SIGNATURES = {
     "qattn_probe_mfma_f16": [_vp, _vp, _vp, _vp],
     "qattn_probe_tr16": [_vp, _vp, _vp],
     "qattn_probe_pk": [_vp, _vp, _vp, _vp],
+    "qattn_probe_fwd_helpers": [_vp] * 7,
 }
 
 _lib = None
@@ -55,7 +56,7 @@ def load(path: os.PathLike | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("QATTN_LIB", LIB_PATH))
     if not p.exists():
         raise QAttnError(
             f"{p} not found: build it with `python -m quantizedattention_amd.build` "

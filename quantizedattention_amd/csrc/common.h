@@ -129,6 +129,68 @@ QA_DEVICE float pair_max(float x) {
 QA_DEVICE void exp2_pk4(const v2h* x, v2h* r) { QA_PK4("v_exp_f16"); }
 QA_DEVICE void trunc_pk4(const v2h* x, v2h* r) { QA_PK4("v_trunc_f16"); }
 
+// d[j] = {f16(a[2j]*c + n), f16(a[2j+1]*c + n)}, one rounding each (v_fma_mix, f32 sources).  All 8
+// low halves are written before the high halves so that no mixhi reads a just-written VGPR.
+QA_DEVICE void fma_mix8(const float* a, float c, float n, v2h* d) {
+  unsigned r[8];
+  asm("v_fma_mixlo_f16 %0, %8, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, %10, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %2, %12, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %3, %14, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %4, %16, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %5, %18, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %6, %20, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %7, %22, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %9, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, %11, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %2, %13, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %3, %15, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %4, %17, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %5, %19, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %6, %21, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %7, %23, %24, %25 op_sel_hi:[0,0,0]"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
+        "=&v"(r[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
+        "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]),
+        "v"(a[15]), "v"(c), "v"(n));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = __builtin_bit_cast(v2h, r[j]);
+}
+// f16(a*c) with one rounding (the same v_fma_mix rounding as fma_mix8, so that a row max computed
+// from the int32 maximum equals the max of the fma_mix8 results bit for bit)
+QA_DEVICE _Float16 mul_mix(float a, float c) {
+  unsigned r;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=v"(r) : "v"(a), "v"(c));
+  return __builtin_bit_cast(v2h, r)[0];
+}
+// y = RTZ_f16(127 e + 1024) = P_i8 + 1024 (exact integer), then w = RNE_f16(y*sp - 1024*sp) =
+// f16(P_i8 * sp).  MODE.FP_ROUND[3:2] (f16/f64) = 3 (toward zero) only around the first 8 ops.
+QA_DEVICE void p_operand8(const v2h* e, v2h sp2, v2h nsp2, v2h* w) {
+  const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
+  const v2h k1024 = {(_Float16)1024.0f, (_Float16)1024.0f};
+  v2h y[8];
+  asm volatile(
+      "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\t"
+      "s_nop 1\n\t"
+      "v_pk_fma_f16 %0, %8, %16, %17\n\t"
+      "v_pk_fma_f16 %1, %9, %16, %17\n\t"
+      "v_pk_fma_f16 %2, %10, %16, %17\n\t"
+      "v_pk_fma_f16 %3, %11, %16, %17\n\t"
+      "v_pk_fma_f16 %4, %12, %16, %17\n\t"
+      "v_pk_fma_f16 %5, %13, %16, %17\n\t"
+      "v_pk_fma_f16 %6, %14, %16, %17\n\t"
+      "v_pk_fma_f16 %7, %15, %16, %17\n\t"
+      "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 0\n\t"
+      "s_nop 1"
+      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(y[4]), "=&v"(y[5]), "=&v"(y[6]),
+        "=&v"(y[7])
+      : "v"(e[0]), "v"(e[1]), "v"(e[2]), "v"(e[3]), "v"(e[4]), "v"(e[5]), "v"(e[6]), "v"(e[7]),
+        "v"(k127), "v"(k1024));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = __builtin_elementwise_fma(y[j], sp2, nsp2);
+}
+
 // LDS-DMA of one 16-B chunk per lane: the LDS destination is lds_base (wave-uniform) + 16*lane.
 // Issued from inline asm on purpose: hipcc cannot tell which LDS bytes a global_load_lds writes, so
 // for the builtin form it inserts s_waitcnt vmcnt(0) before every later ds_read (serialising the
@@ -145,10 +207,25 @@ QA_DEVICE void glds16(const void* gsrc, void* lds_base) {
       : "v"(gsrc), "s"(lds)
       : "memory");
 }
+// LDS-DMA with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset (global SADDR
+// form): no per-lane 64-bit address arithmetic in the loop.
+QA_DEVICE void glds16_s(const void* sbase, unsigned voff, void* lds_base) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(lds_base));
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
 // s_waitcnt vmcnt(0) as a real instruction hipcc's waitcnt pass understands: retire every ordinary
 // global load before a loop that issues asm LDS-DMA (otherwise the compiler's first-use wait for
 // those loads lands inside the loop and also waits for the in-flight DMA).
 QA_DEVICE void vmem_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// Wait for every outstanding VMEM op of this wave (e.g. LDS-DMA still landing before the wave exits).
+QA_DEVICE void vmcnt_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // Wait for every outstanding VMEM op of this wave (incl. LDS-DMA) and LDS op, then barrier.
 QA_DEVICE void dma_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

@@ -83,3 +83,31 @@ extern "C" int qattn_probe_pk(const void* x, void* e, void* t, void* stream) {
                      (v2h*)e, (v2h*)t);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// int8-forward softmax helpers: w = p_operand8(e, sp) and d = fma_mix8(a, c, n), 16 lanes x 8 pairs
+namespace qattn {
+__global__ void probe_fwd_helpers_kernel(const v2h* e, const _Float16* sp, v2h* w, const float* a,
+                                         const float* cn, v2h* d) {
+  const int i = threadIdx.x;
+  if (i >= 16) return;
+  v2h ei[8], wo[8], dd[8];
+  for (int j = 0; j < 8; ++j) ei[j] = e[8 * i + j];
+  const _Float16 s = sp[i];
+  const v2h sp2 = {s, s};
+  const _Float16 ns = (_Float16)(-1024.0f) * s;
+  const v2h nsp2 = {ns, ns};
+  p_operand8(ei, sp2, nsp2, wo);
+  for (int j = 0; j < 8; ++j) w[8 * i + j] = wo[j];
+  float af[16];
+  for (int j = 0; j < 16; ++j) af[j] = a[16 * i + j];
+  fma_mix8(af, cn[2 * i], cn[2 * i + 1], dd);
+  for (int j = 0; j < 8; ++j) d[8 * i + j] = dd[j];
+}
+}  // namespace qattn
+extern "C" int qattn_probe_fwd_helpers(const void* e, const void* sp, void* w, const void* a,
+                                       const void* cn, void* d, void* stream) {
+  hipLaunchKernelGGL(probe_fwd_helpers_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (const v2h*)e, (const _Float16*)sp, (v2h*)w, (const float*)a, (const float*)cn,
+                     (v2h*)d);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

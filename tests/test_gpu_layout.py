@@ -55,3 +55,27 @@ def test_packed_half_helpers(lib):
     torch.cuda.synchronize()
     assert torch.allclose(e.cpu().float(), torch.exp2(x.float()), rtol=2e-3, atol=0)
     assert torch.equal(t.cpu().float(), torch.trunc((x * 127).float()))
+
+
+def test_int8_fwd_softmax_helpers(lib):
+    """p_operand8: f16(trunc(127 e) * sp) via the round-toward-zero packed fma (bit-exact);
+    fma_mix8: f16(a*c + n) with one rounding (bit-exact vs an fp64 reference rounded to f16)."""
+    from quantizedattention_amd import _lib
+    g = torch.Generator().manual_seed(5)
+    e = torch.rand(256, generator=g).half()
+    e[::17] = 1.0          # the row maximum: 127 exactly
+    e[5] = 0.0
+    sp = (torch.rand(16, generator=g) * 2 + 1e-3).half()
+    a = (torch.randn(256, generator=g) * 3e5).round()
+    cn = torch.stack([torch.rand(16, generator=g) * 1e-4, -torch.rand(16, generator=g) * 8], 1).float()
+    ed, spd, ad, cnd = e.cuda(), sp.cuda(), a.cuda(), cn.reshape(-1).cuda()
+    w = torch.empty(256, dtype=torch.float16, device="cuda")
+    d = torch.empty(256, dtype=torch.float16, device="cuda")
+    _lib.call("qattn_probe_fwd_helpers", _lib.ptr(ed), _lib.ptr(spd), _lib.ptr(w), _lib.ptr(ad),
+              _lib.ptr(cnd), _lib.ptr(d), _lib.stream_of(ed))
+    torch.cuda.synchronize()
+    lane = torch.arange(256) // 16
+    exp_w = (torch.trunc(e.double() * 127) * sp[lane].double()).half()
+    assert torch.equal(w.cpu().view(torch.int16), exp_w.view(torch.int16))
+    exp_d = (a.double() * cn[lane, 0].double() + cn[lane, 1].double()).half()
+    assert torch.equal(d.cpu().view(torch.int16), exp_d.view(torch.int16))
