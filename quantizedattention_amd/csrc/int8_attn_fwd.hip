@@ -35,6 +35,10 @@
 
 namespace qattn {
 
+#ifndef QA_FWD_OCC
+#define QA_FWD_OCC 3
+#endif
+
 template <int D>
 struct Int8FwdCfg {
   static constexpr int WAVES = 4;
@@ -130,7 +134,7 @@ struct SmTile {
 // 2 = no PV MFMA, 3 = no QK^T MFMA, 4 = no K/V streaming (ring slot 0 reused, no barriers),
 // 5 = 4 + no softmax.  Outputs of AB != 0 are meaningless.
 template <int D, int AB = 0>
-__global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
+__global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
     const _Float16* __restrict__ sk, const _Float16* __restrict__ vdq, _Float16* __restrict__ out,
     _Float16* __restrict__ lse, int BH, int S, float qks) {
@@ -292,24 +296,46 @@ __global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
       for (int j = 0; j < 4; ++j) pw[s][j] = __builtin_bit_cast(unsigned, w[4 * s + j]);
   };
 
-  // O^T += Vdq^T P^T for tile t
-  auto pv = [&](int t, const v4u* pw) {
+  // O^T += Vdq^T P^T for tile t: operand loads (issued early, consumed after QK(t+1) and SM2(t))
+  // and the MFMAs
+  auto pv_load = [&](int t, v8h* va) {
     const char* vl = slot_of(t);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b) {
-        const char* va = vl + voff[b] + 16 * s * 2 * D;
-        const v8h a = __builtin_bit_cast(v8h, ds_read_tr16_x2(va, va + 8 * 2 * D));
+        const char* a = vl + voff[b] + 16 * s * 2 * D;
+        va[s * C::NDB + b] = __builtin_bit_cast(v8h, ds_read_tr16_x2(a, a + 8 * 2 * D));
+      }
+  };
+  auto pv_mma = [&](const v8h* va, const v4u* pw) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < C::NDB; ++b) {
         if constexpr (AB == 2) {
-          asm volatile("" ::"v"(a), "v"(pw[s]));
+          asm volatile("" ::"v"(va[s * C::NDB + b]), "v"(pw[s]));
         } else {
-          o[b] = mfma_f16(a, __builtin_bit_cast(v8h, pw[s]), o[b]);
+          o[b] = mfma_f16(va[s * C::NDB + b], __builtin_bit_cast(v8h, pw[s]), o[b]);
         }
       }
-    }
   };
 
+#if defined(QA_FWD_PRIO)
+  {  // co-resident workgroups (blocks b, b+256, b+512 on one CU in the first wave of dispatch) get
+     // different static priorities so that their identical streams do not run in lockstep
+    const int pr = (blockIdx.x >> 8) % 3;
+    if (pr == 1) __builtin_amdgcn_s_setprio(1);
+    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+  }
+#endif
+#if defined(QA_FWD_SLEEP)
+  {
+    const int pr = (blockIdx.x >> 8) % 3;
+    if (pr == 1) __builtin_amdgcn_s_sleep(QA_FWD_SLEEP);
+    else if (pr == 2) { __builtin_amdgcn_s_sleep(QA_FWD_SLEEP); __builtin_amdgcn_s_sleep(QA_FWD_SLEEP); }
+  }
+#endif
   vmem_drain();
   __syncthreads();
 
@@ -324,12 +350,18 @@ __global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
   // harmless (its row max cannot move m) and it keeps the loop body branch-free.
   for (int t = 0; t < nt; ++t) {
     if constexpr (STREAM) {
+#if defined(QA_FWD_NOBAR)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::IPW) : "memory");   // timing experiment only
+#else
       ring_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
+#endif
       dma.issue(kbase, vbase, smem + ((t + 3) & 3) * C::SLOT, min(t + 3, nt - 1));
     }
     if (active) {
       const int tn = min(t + 1, nt - 1);
       const float cn = cq * (float)sk_lds[tn];
+      v8h va[2 * C::NDB];
+      pv_load(t, va);
       const v16i nacc = qk(tn);
       v4u pw[2];
       if constexpr (SOFTMAX) {
@@ -340,7 +372,7 @@ __global__ __launch_bounds__(256, 3) void int8_attn_fwd_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) pw[s][j] = __builtin_bit_cast(unsigned, st.d[4 * s + j]) & 0x3fff3fffu;
       }
-      pv(t, pw);
+      pv_mma(va, pw);
       if constexpr (SOFTMAX) {
         const _Float16 rm = sm1a(nacc, cn, st);
         sm1b(rm, st);

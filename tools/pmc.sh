@@ -1,7 +1,7 @@
 #!/bin/bash
 # usage: tools/pmc.sh <kernel_runner name> <outdir>   (runs on the GPU box; separate --pmc passes)
 set -e
-NAME=$1; OUT=$2
+NAME=$1; OUT=$(realpath -m $2)
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT

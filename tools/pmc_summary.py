@@ -17,7 +17,7 @@ for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
         vals[c].append(v)
 avg = {c: sum(v) / len(v) for c, v in vals.items()}
 dur = []
-for row in csv.DictReader(open(glob.glob(f"{root}/trace/run_kernel_trace.csv")[0])):
+for row in csv.DictReader(open(glob.glob(f"{root}/trace/**/*kernel_trace.csv", recursive=True)[0])):
     if pat in row["Kernel_Name"]:
         dur.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
 avg["duration_ns"] = sum(dur) / len(dur) if dur else None
