@@ -44,16 +44,16 @@ QA_DEVICE v16f mfma_bf16(v8bf a, v8bf b, v16f c) {
 }
 
 // ---------------------------------------------------------------- conversions
-// Round-to-nearest-even packs (gfx950 VOP3 v_cvt_pk_{f16,bf16}_f32).
+// Round-to-nearest-even packs (gfx950 v_cvt_pk_{f16,bf16}_f32, emitted by hipcc for these vector
+// conversions).  Deliberately NOT inline asm: the results feed MFMA operands, and hipcc inserts the
+// VALU-write -> MFMA-read wait states only for producers it can see.
+typedef __bf16 v2bf_ __attribute__((ext_vector_type(2)));
+typedef float v2f_ __attribute__((ext_vector_type(2)));
 QA_DEVICE unsigned pk_f16(float lo, float hi) {
-  unsigned r;
-  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((v2f_{lo, hi}), v2h));
 }
 QA_DEVICE unsigned pk_bf16(float lo, float hi) {
-  unsigned r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((v2f_{lo, hi}), v2bf_));
 }
 QA_DEVICE float bf16_bits_to_f32(unsigned short b) { return __uint_as_float(((unsigned)b) << 16); }
 // RNE f32 -> bf16 -> f32 (value rounding only).
@@ -219,6 +219,26 @@ QA_DEVICE void glds16_s(const void* sbase, unsigned voff, void* lds_base) {
       : "=&s"(keep)
       : "v"(voff), "s"(sbase), "s"(lds)
       : "memory");
+}
+// dword LDS-DMA (64 lanes x 4 B = 256 B, lane-linear destination), SADDR form
+QA_DEVICE void glds4_s(const void* sbase, unsigned voff, void* lds_base) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(lds_base));
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
+// LDS-ring step: wait until at most N of this wave's VMEM ops (the LDS-DMA of later tiles) are in
+// flight and all its LDS reads returned, then workgroup barrier (publishes the landed tile and
+// frees the oldest slot).
+template <int N>
+QA_DEVICE void ring_wait_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 // s_waitcnt vmcnt(0) as a real instruction hipcc's waitcnt pass understands: retire every ordinary
 // global load before a loop that issues asm LDS-DMA (otherwise the compiler's first-use wait for

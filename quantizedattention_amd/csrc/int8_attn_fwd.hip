@@ -113,13 +113,6 @@ struct DmaPlan {
   }
 };
 
-// wait until at most N of this wave's VMEM ops (the LDS-DMA of later tiles) are in flight and all
-// LDS reads returned, then workgroup barrier (publishes the landed tile, frees the oldest slot)
-template <int N>
-QA_DEVICE void ring_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
 // (compiles to v_max3_i32).  Deliberately NOT inline asm: its inputs are MFMA results, and hipcc's
 // hazard recogniser inserts the MFMA-result -> VALU wait states only for instructions it emits itself.
 QA_DEVICE int imax3(int a, int b, int c) { return max(max(a, b), c); }
@@ -353,7 +346,7 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
 #if defined(QA_FWD_NOBAR)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::IPW) : "memory");   // timing experiment only
 #else
-      ring_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
+      ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
 #endif
       dma.issue(kbase, vbase, smem + ((t + 3) & 3) * C::SLOT, min(t + 3, nt - 1));
     }

@@ -34,74 +34,17 @@ namespace qattn {
 template <int D>
 struct I8BwdCfg {
   static constexpr int NKS8 = D / 32;    // i8 k-steps over D
-  static constexpr int NDB = D / 32;
+  static constexpr int NDB = D / 32;     // 32-wide d blocks of the accumulators
   static constexpr int T8 = 32 * D;      // 32-row int8 tile bytes
   static constexpr int T16 = 64 * D;     // 32-row bf16 tile bytes
-  // kernel A stage: Q8, O8 (int8 rows), QB, OB (bf16 tr), LD (32 x {lse, D} f32)
-  static constexpr int A_STAGE = 2 * T8 + 2 * T16 + 256;
-  static constexpr int A_INST = (2 * T8 + 2 * T16) / 1024 + 1;   // + 1 dword-DMA for LD
-  static constexpr int A_IPW = (A_INST + 3) / 4;                  // per wave (padded)
-  // kernel A split by output (MODE 1 = dV only: Q8, OB, LD; MODE 2 = dK only: Q8, O8, QB, LD)
-  static constexpr int A1_STAGE = T8 + T16 + 256;
-  static constexpr int A1_IPW = ((T8 + T16) / 1024 + 1 + 3) / 4;
-  static constexpr int A2_STAGE = 2 * T8 + T16 + 256;
-  static constexpr int A2_IPW = ((2 * T8 + T16) / 1024 + 1 + 3) / 4;
-  // kernel B stage: K8, V8 (int8 rows), KB (bf16 tr)
-  static constexpr int B_STAGE = 2 * T8 + T16;
-  static constexpr int B_INST = B_STAGE / 1024;
-  static constexpr int B_IPW = B_INST / 4;
 };
+// LDS image swizzles: int8 rows (read by rows for the int8 MFMAs) and bf16 tr images (read by
+// ds_read_b64_tr_b16 for the bf16 MFMAs); conflict-free for both access patterns.
 template <int D>
 QA_DEVICE int i8_sw(int row) { return (row >> ((D == 128) ? 1 : 2)) & (D / 16 - 1); }
 template <int D>
 QA_DEVICE int t16_sw(int row) { return (row & 3) << ((D == 128) ? 2 : 1); }
 
-// Global chunk that lands at LDS position (row, p) of a swizzled image with `nch` 16-B chunks/row.
-template <int D, bool TR>
-QA_DEVICE int src_chunk(int row, int p) { return p ^ (TR ? t16_sw<D>(row) : i8_sw<D>(row)); }
-
-// LDS-DMA of instruction `inst` (1 KiB) of a 32-row tile: rows of RB bytes at gsrc (row stride RB).
-template <int D, int RB, bool TR>
-QA_DEVICE void dma_tile_inst(const char* gsrc, char* lds_tile, int inst, int lane) {
-  constexpr int NCH = RB / 16, RPI = 64 / NCH;
-  const int row = inst * RPI + lane / NCH, p = lane % NCH;
-  glds16(gsrc + (long)row * RB + 16 * src_chunk<D, TR>(row, p), lds_tile + inst * 1024);
-}
-// dword LDS-DMA (64 lanes x 4 B = 256 B, lane-linear)
-QA_DEVICE void glds4(const void* gsrc, void* lds_base) {
-  const unsigned lds = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(lds_base));
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds)
-      : "memory");
-}
-template <int N>
-QA_DEVICE void vmcnt_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// A operand (X^T, 32 d x 16 rows) of a 32x32x16 product from a bf16 [row][d] tr image.
-template <int D>
-QA_DEVICE v8bf t16_frag(const char* base, int row_base, int b, int lane) {
-  const int h = lane >> 5, gg = (lane >> 4) & 1, i16 = lane & 15;
-  const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
-  const int row = row_base + 4 * h + (i16 >> 2);
-  const int ch = d / 8, within = (d % 8) * 2;
-  return __builtin_bit_cast(
-      v8bf, ds_read_tr16_x2(base + row * 2 * D + 16 * (ch ^ t16_sw<D>(row)) + within,
-                            base + (row + 8) * 2 * D + 16 * (ch ^ t16_sw<D>(row + 8)) + within));
-}
-QA_DEVICE float max16_abs(const float* x) {
-  float m0 = vmax(fabsf(x[0]), fabsf(x[1])), m1 = vmax(fabsf(x[2]), fabsf(x[3]));
-  float m2 = vmax(fabsf(x[4]), fabsf(x[5])), m3 = vmax(fabsf(x[6]), fabsf(x[7]));
-  float m4 = vmax(fabsf(x[8]), fabsf(x[9])), m5 = vmax(fabsf(x[10]), fabsf(x[11]));
-  float m6 = vmax(fabsf(x[12]), fabsf(x[13])), m7 = vmax(fabsf(x[14]), fabsf(x[15]));
-  return vmax(vmax(vmax(m0, m1), vmax(m2, m3)), vmax(vmax(m4, m5), vmax(m6, m7)));
-}
 // Quantise 16 values with the tile scale and emit the bf16 operand  trunc(x / s) * c.
 QA_DEVICE void quant_operand(const float* x, float inv, float c, v8bf* out) {
 #pragma unroll
@@ -160,135 +103,206 @@ __global__ __launch_bounds__(256) void i8_to_bf16_kernel(const int8_t* __restric
   reinterpret_cast<v4u*>(y)[2 * i + 1] = hi;
 }
 
-// ------------------------------------------------------------------------- kernel A: dK, dV
-// MODE 0: dK and dV in one pass (1 wave/SIMD: 2 x 64 fp32 accumulator registers);
-// MODE 1: dV only (S -> P -> P_i8 operand);  MODE 2: dK only (S, dP -> dS -> dS_i8 operand).
-// The split pair re-computes S (4 extra int8 MFMAs per tile) but halves the accumulator registers,
-// so each kernel runs at 2-3 waves per SIMD.
-template <int D, int MODE>
-struct AStage {
+// ------------------------------------------------------------------ dV, dK, dQ: one kernel template
+// Every backward product has the same shape.  A wave owns 32 rows of one side X (keys for dV/dK,
+// queries for dQ) whose int8 fragments stay in registers, and streams 32-row tiles of the other
+// side Y through a 4-slot LDS ring (LDS-DMA, SADDR form, lane-constant swizzled source offsets):
+//   ROLE_DV: X = K           Y = {Q8, dO image, LD}      S          -> P  -> dV += dO^T P
+//   ROLE_DK: X = K, V        Y = {Q8, dO8, q image, LD}  S, dP      -> dS -> dK += q^T dS
+//   ROLE_DQ: X = Q, dO       Y = {K8, V8, k image}       S, dP      -> dS -> dQ += k^T dS^T
+// S and dP are int8 MFMAs (32x32x32) on the quantised operands; P = exp2(S*c1 - lse) and
+// dS = P*(dP*c2 - D) in fp32 (c1 = sq*(sk*qks), c2 = sdO*sv, identical in all three kernels so the
+// per-tile quantisation of P and dS is the same everywhere); P / dS are quantised per 32x32 tile
+// (amax/127, trunc, int8:363-365, 403-405) and enter a bf16 32x32x16 MFMA as the exact bf16 value
+// trunc(x/s) * s * s_other, against the exact bf16 image of the other int8 operand.
+// Software pipeline by one tile: the int8 MFMAs of tile t+1 are issued before the quantisation of
+// tile t, and the fp32 P/dS of tile t+1 are computed beside the bf16 MFMAs of tile t.
+enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2 };
+
+template <int D, int ROLE>
+struct BwdCfg {
   using C = I8BwdCfg<D>;
-  static constexpr bool NEED_O8 = MODE != 1, NEED_QB = MODE != 1, NEED_OB = MODE != 2;
-  static constexpr int Q8 = 0;
-  static constexpr int O8 = Q8 + C::T8;
-  static constexpr int QB = O8 + (NEED_O8 ? C::T8 : 0);
-  static constexpr int OB = QB + (NEED_QB ? C::T16 : 0);
-  static constexpr int LDO = OB + (NEED_OB ? C::T16 : 0);
-  static constexpr int BYTES = LDO + 256;
-  static constexpr int N8 = C::T8 / 1024, N16 = C::T16 / 1024;
-  static constexpr int INST = N8 + (NEED_O8 ? N8 : 0) + (NEED_QB ? N16 : 0) + (NEED_OB ? N16 : 0) + 1;
+  static constexpr bool TWO = ROLE != ROLE_DV;     // S and dP (else S only)
+  static constexpr bool HAS_LD = ROLE != ROLE_DQ;  // per-row {lse, D} of the streamed side
+  static constexpr int Y8A = 0;
+  static constexpr int Y8B = C::T8;
+  static constexpr int TR = TWO ? 2 * C::T8 : C::T8;
+  static constexpr int LDO = TR + C::T16;
+  static constexpr int SLOT = LDO + (HAS_LD ? 256 : 0);
+  static constexpr int NSLOT = 4;
+  static constexpr int NP8 = C::T8 / 1024, NP16 = C::T16 / 1024;
+  static constexpr int INST = NP8 * (TWO ? 2 : 1) + NP16 + (HAS_LD ? 1 : 0);
   static constexpr int IPW = (INST + 3) / 4;
 };
 
-template <int D, int MODE>
-__global__ __launch_bounds__(256, MODE == 0 ? 1 : 2) void int8_bwd_dkdv_kernel(
-    const int8_t* __restrict__ dOi, const _Float16* __restrict__ sdO, const int8_t* __restrict__ qi,
-    const _Float16* __restrict__ sq, const int8_t* __restrict__ ki, const _Float16* __restrict__ sk,
-    const int8_t* __restrict__ vi, const _Float16* __restrict__ sv, const float2* __restrict__ LD,
-    const __bf16* __restrict__ qb, const __bf16* __restrict__ ob, _Float16* __restrict__ dk,
-    _Float16* __restrict__ dv, int BH, int S, float qks, float sms) {
+// LDS-DMA plan: per wave slot i (IPW of them) the region it fills (0 = Y8A, 1 = Y8B, 2 = TR, 3 = LD),
+// its lane-constant source byte offset inside the region's tile and its LDS offset inside the slot.
+template <int D, int ROLE>
+struct BwdDma {
+  using G = BwdCfg<D, ROLE>;
+  unsigned voff[G::IPW];
+  int lds_off[G::IPW];
+  int reg[G::IPW];
+  const char* base[G::IPW];   // region tensor of the slot (head row 0) and its per-tile stride
+  int stride[G::IPW];
+  QA_DEVICE void init(int wave, int lane, const char* y8a, const char* y8b, const char* tr,
+                      const char* ld) {
+#pragma unroll
+    for (int i = 0; i < G::IPW; ++i) {
+      int p = wave + 4 * i;
+      if (p >= G::INST) p = wave;   // padding slot: re-issue the wave's first piece (same bytes)
+      if (p < G::NP8) {
+        set_i8(i, 0, G::Y8A, p, lane);
+        base[i] = y8a;
+      } else if (G::TWO && p < 2 * G::NP8) {
+        set_i8(i, 1, G::Y8B, p - G::NP8, lane);
+        base[i] = y8b;
+      } else {
+        const int q = p - (G::TWO ? 2 : 1) * G::NP8;
+        if (q < G::NP16) {
+          constexpr int NCH = 2 * D / 16, RPI = 64 / NCH;
+          const int row = q * RPI + lane / NCH, c = lane % NCH;
+          voff[i] = row * 2 * D + 16 * (c ^ t16_sw<D>(row));
+          lds_off[i] = G::TR + q * 1024;
+          reg[i] = 2;
+          base[i] = tr;
+          stride[i] = 64 * D;
+        } else {
+          voff[i] = 4 * lane;
+          lds_off[i] = G::LDO;
+          reg[i] = 3;
+          base[i] = ld;
+          stride[i] = 256;
+        }
+      }
+    }
+  }
+  QA_DEVICE void set_i8(int i, int r, int region, int piece, int lane) {
+    constexpr int NCH = D / 16, RPI = 64 / NCH;
+    const int row = piece * RPI + lane / NCH, c = lane % NCH;
+    voff[i] = row * D + 16 * (c ^ i8_sw<D>(row));
+    lds_off[i] = region + piece * 1024;
+    reg[i] = r;
+    stride[i] = 32 * D;
+  }
+  QA_DEVICE void issue(char* slot, int t) const {
+#pragma unroll
+    for (int i = 0; i < G::IPW; ++i) {
+      const char* b = base[i] + (long)t * stride[i];
+      if (reg[i] == 3) glds4_s(b, voff[i], slot + lds_off[i]);
+      else glds16_s(b, voff[i], slot + lds_off[i]);
+    }
+  }
+};
+
+// max over |x| of 16 values (v_max3_f32 with abs modifiers)
+QA_DEVICE float max16_abs3(const float* x) {
+  float m = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fabsf(x[2]));
+#pragma unroll
+  for (int i = 3; i < 15; i += 2) m = fmaxf(fmaxf(m, fabsf(x[i])), fabsf(x[i + 1]));
+  return fmaxf(m, fabsf(x[15]));
+}
+
+template <int D, int ROLE>
+__global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
+    const int8_t* __restrict__ x8a, const int8_t* __restrict__ x8b, const _Float16* __restrict__ sxa,
+    const _Float16* __restrict__ sxb, const int8_t* __restrict__ y8a, const int8_t* __restrict__ y8b,
+    const __bf16* __restrict__ ytr, const float2* __restrict__ yld, const _Float16* __restrict__ sya,
+    const _Float16* __restrict__ syb, const float2* __restrict__ xld, _Float16* __restrict__ out,
+    int BH, int S, float qks, float sms) {
   using C = I8BwdCfg<D>;
-  using G = AStage<D, MODE>;
-  constexpr bool DO_DV = MODE != 2, DO_DK = MODE != 1;
+  using G = BwdCfg<D, ROLE>;
+  constexpr bool TWO = G::TWO;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nkb = (S + 127) / 128;
-  int bh, kt;
-  xcd_remap(blockIdx.x, nkb, BH, bh, kt);
+  const int nxb = (S + 127) / 128;
+  int bh, xt;
+  xcd_remap(blockIdx.x, nxb, BH, bh, xt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const int k0 = kt * 128 + wave * 32;
-  const bool active = k0 < S;
+  const int x0 = xt * 128 + wave * 32;
+  const bool active = x0 < S;
   const long hrow = (long)bh * S;
-  const int nqt = S / 32;
+  const int nt = S / 32;
 
-  // one q-tile stage: wave w issues DMA slots w, w+4, ...; slots past the real instructions repeat
-  // the LD dword DMA (same bytes, benign) so that every wave issues exactly G::IPW (counted vmcnt).
-  auto stage = [&](int t, int buf) {
-    t = min(t, nqt - 1);
-    const long r0 = hrow + 32L * t;
-    char* base = smem + buf * G::BYTES;
-    for (int i = 0; i < G::IPW; ++i) {
-      int inst = wave + 4 * i;
-      if (inst < G::N8) {
-        dma_tile_inst<D, D, false>(reinterpret_cast<const char*>(qi + r0 * D), base + G::Q8, inst, lane);
-        continue;
-      }
-      inst -= G::N8;
-      if constexpr (G::NEED_O8) {
-        if (inst < G::N8) {
-          dma_tile_inst<D, D, false>(reinterpret_cast<const char*>(dOi + r0 * D), base + G::O8, inst, lane);
-          continue;
-        }
-        inst -= G::N8;
-      }
-      if constexpr (G::NEED_QB) {
-        if (inst < G::N16) {
-          dma_tile_inst<D, 2 * D, true>(reinterpret_cast<const char*>(qb + r0 * D), base + G::QB, inst, lane);
-          continue;
-        }
-        inst -= G::N16;
-      }
-      if constexpr (G::NEED_OB) {
-        if (inst < G::N16) {
-          dma_tile_inst<D, 2 * D, true>(reinterpret_cast<const char*>(ob + r0 * D), base + G::OB, inst, lane);
-          continue;
-        }
-      }
-      glds4(reinterpret_cast<const char*>(LD + r0) + 4 * lane, base + G::LDO);
-    }
-  };
-  stage(0, 0);
-  stage(1, 1);
-  // per-tile q / dO scales of the head, once, in LDS (a vector global load inside the loop would
-  // make hipcc wait vmcnt for the in-flight LDS-DMA)
-  _Float16* sc_lds = reinterpret_cast<_Float16*>(smem + 3 * G::BYTES);
-  for (int i = tid; i < nqt; i += 256) {
-    sc_lds[i] = sq[hrow / 32 + i];
-    sc_lds[nqt + i] = sdO[hrow / 32 + i];
+  const char* gy8a = reinterpret_cast<const char*>(y8a + hrow * D);
+  const char* gy8b = reinterpret_cast<const char*>(y8b + hrow * D);
+  const char* gytr = reinterpret_cast<const char*>(ytr + hrow * D);
+  const char* gyld = reinterpret_cast<const char*>(yld + hrow);
+  BwdDma<D, ROLE> dma;
+  dma.init(wave, lane, gy8a, gy8b, gytr, gyld);
+  dma.issue(smem, 0);
+  dma.issue(smem + G::SLOT, min(1, nt - 1));
+  dma.issue(smem + 2 * G::SLOT, min(2, nt - 1));
+  // per-tile scales of the streamed side, once, in LDS (a global load inside the loop would make
+  // hipcc wait vmcnt for the in-flight LDS-DMA)
+  _Float16* sc_lds = reinterpret_cast<_Float16*>(smem + G::NSLOT * G::SLOT);
+  for (int i = tid; i < nt; i += 256) {
+    sc_lds[i] = sya[hrow / 32 + i];
+    sc_lds[nt + i] = syb[hrow / 32 + i];
   }
 
-  v4i kfr[C::NKS8], vfr[C::NKS8];
-  float skw = 0.f, svw = 0.f;
+  // own-side int8 fragments (B operands): lane holds X[x0 + c32][32s + 16h .. +16]
+  v4i xa[C::NKS8], xb[C::NKS8];
+  float sxaw = 0.f, sxbw = 0.f, lsex = 0.f, Dx = 0.f;
   if (active) {
-    const int8_t* kr = ki + (hrow + k0 + c32) * D + 16 * h;
-    const int8_t* vr = vi + (hrow + k0 + c32) * D + 16 * h;
+    const long r = hrow + x0 + c32;
 #pragma unroll
     for (int s = 0; s < C::NKS8; ++s) {
-      kfr[s] = *reinterpret_cast<const v4i*>(kr + 32 * s);
-      if constexpr (DO_DK) vfr[s] = *reinterpret_cast<const v4i*>(vr + 32 * s);
+      xa[s] = *reinterpret_cast<const v4i*>(x8a + r * D + 16 * h + 32 * s);
+      if constexpr (TWO) xb[s] = *reinterpret_cast<const v4i*>(x8b + r * D + 16 * h + 32 * s);
     }
-    skw = (float)sk[(hrow + k0) / 32];
-    svw = (float)sv[(hrow + k0) / 32];
+    sxaw = (float)sxa[(hrow + x0) / 32];
+    sxbw = (float)sxb[(hrow + x0) / 32];
+    if constexpr (!G::HAS_LD) {
+      const float2 v = xld[r];
+      lsex = v.x;
+      Dx = v.y;
+    }
   }
-  const float ck = skw * qks;
-  v16f dka[C::NDB], dva[C::NDB];
-#pragma unroll
-  for (int b = 0; b < C::NDB; ++b) { dka[b] = v16f{}; dva[b] = v16f{}; }
-  int roff[C::NKS8];
+  // lane-constant LDS offsets: int8 A-operand rows, tr-image A-operand (per 32-wide d block)
+  int roff[C::NKS8], troff[C::NDB];
 #pragma unroll
   for (int s = 0; s < C::NKS8; ++s) roff[s] = c32 * D + 16 * ((2 * s + h) ^ i8_sw<D>(c32));
-
-  vmem_drain();
-  vmcnt_wait<0>();
-  __syncthreads();
-  for (int t = 0; t < nqt; ++t) {
-    const int buf = t % 3;
-    stage(t + 2, (t + 2) % 3);
-    const char* base = smem + buf * G::BYTES;
-    const float* ld = reinterpret_cast<const float*>(base + G::LDO);
-    const float sqt = (float)sc_lds[t];
-    const float sdt = (float)sc_lds[nqt + t];
-    if (active) {
-      v16i sacc = v16i{}, pacc = v16i{};
+  {
+    const int gg = (lane >> 4) & 1, i16 = lane & 15;
+    const int row = 4 * h + (i16 >> 2);
 #pragma unroll
-      for (int s = 0; s < C::NKS8; ++s) {
-        sacc = mfma_i8(*reinterpret_cast<const v4i*>(base + G::Q8 + roff[s]), kfr[s], sacc);
-        if constexpr (DO_DK)
-          pacc = mfma_i8(*reinterpret_cast<const v4i*>(base + G::O8 + roff[s]), vfr[s], pacc);
-      }
-      const float c1 = sqt * ck, c2 = sdt * svw;
-      float P[16], dS[16];
+    for (int b = 0; b < C::NDB; ++b) {
+      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
+      troff[b] = G::TR + row * 2 * D + 16 * ((d / 8) ^ t16_sw<D>(row)) + (d % 8) * 2;
+    }
+  }
+  v16f acc[C::NDB];
+#pragma unroll
+  for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
+
+  auto slot = [&](int t) -> const char* { return smem + (t & 3) * G::SLOT; };
+  // int8 products of tile t: S (and dP)
+  auto products = [&](int t, v16i& sa, v16i& pa) {
+    const char* base = slot(t);
+    sa = v16i{};
+    pa = v16i{};
+#pragma unroll
+    for (int s = 0; s < C::NKS8; ++s) {
+      sa = mfma_i8(*reinterpret_cast<const v4i*>(base + G::Y8A + roff[s]), xa[s], sa);
+      if constexpr (TWO) pa = mfma_i8(*reinterpret_cast<const v4i*>(base + G::Y8B + roff[s]), xb[s], pa);
+    }
+  };
+  // fp32 P (DV) or dS (DK, DQ) of tile t
+  auto values = [&](int t, const v16i& sa, const v16i& pa, float* X) {
+    // c1 = sq*(sk*qks), c2 = sdO*sv with the streamed / own roles of each kernel
+    const float sy_a = (float)sc_lds[t], sy_b = (float)sc_lds[nt + t];
+    float c1, c2;
+    if constexpr (ROLE == ROLE_DQ) {
+      c1 = sxaw * (sy_a * qks);
+      c2 = sxbw * sy_b;
+    } else {
+      c1 = sy_a * (sxaw * qks);
+      c2 = sy_b * sxbw;
+    }
+    if constexpr (G::HAS_LD) {
+      const float* ld = reinterpret_cast<const float*>(slot(t) + G::LDO);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const v4f a = *reinterpret_cast<const v4f*>(ld + 2 * (8 * g + 4 * h));
@@ -298,178 +312,80 @@ __global__ __launch_bounds__(256, MODE == 0 ? 1 : 2) void int8_bwd_dkdv_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
-          P[i] = exp2_f32(fmaf((float)sacc[i], c1, -lse_r[j]));
-          if constexpr (DO_DK) dS[i] = P[i] * fmaf((float)pacc[i], c2, -d_r[j]);
+          const float P = exp2_f32(fmaf((float)sa[i], c1, -lse_r[j]));
+          if constexpr (TWO) X[i] = P * fmaf((float)pa[i], c2, -d_r[j]);
+          else X[i] = P;
         }
       }
-      if constexpr (DO_DV) {
-        const float pmax = wave_max_dpp(max16_abs(P));
-        const float sP = pmax * (1.0f / 127.0f);
-        v8bf pb[2];
-        quant_operand(P, sP > 0.f ? 127.0f / pmax : 0.f, sP * sdt, pb);
+    } else {
 #pragma unroll
-        for (int b = 0; b < C::NDB; ++b)
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-            dva[b] = mfma_bf16(t16_frag<D>(base + G::OB, 16 * s, b, lane), pb[s], dva[b]);
-      }
-      if constexpr (DO_DK) {
-        const float smax = wave_max_dpp(max16_abs(dS));
-        const float ssd = smax * (1.0f / 127.0f);
-        v8bf sb[2];
-        quant_operand(dS, ssd > 0.f ? 127.0f / smax : 0.f, ssd * sqt, sb);
-#pragma unroll
-        for (int b = 0; b < C::NDB; ++b)
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-            dka[b] = mfma_bf16(t16_frag<D>(base + G::QB, 16 * s, b, lane), sb[s], dka[b]);
-      }
-    }
-    vmcnt_wait<G::IPW>();   // tile t+1 (issued last iteration) has landed; t+2 may be in flight
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  vmcnt_wait<0>();
-  if (!active) return;
-  const long krow = hrow + k0 + c32;
-#pragma unroll
-  for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      v4h wk, wv;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        wk[j] = (_Float16)(dka[b][4 * g + j] * sms);
-        wv[j] = (_Float16)dva[b][4 * g + j];
-      }
-      if constexpr (DO_DK) *reinterpret_cast<v4h*>(dk + krow * D + 32 * b + 8 * g + 4 * h) = wk;
-      if constexpr (DO_DV) *reinterpret_cast<v4h*>(dv + krow * D + 32 * b + 8 * g + 4 * h) = wv;
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------- kernel B: dQ
-template <int D>
-__global__ __launch_bounds__(256, 2) void int8_bwd_dq_kernel(
-    const int8_t* __restrict__ dOi, const _Float16* __restrict__ sdO, const int8_t* __restrict__ qi,
-    const _Float16* __restrict__ sq, const int8_t* __restrict__ ki, const _Float16* __restrict__ sk,
-    const int8_t* __restrict__ vi, const _Float16* __restrict__ sv, const float2* __restrict__ LD,
-    const __bf16* __restrict__ kb16, _Float16* __restrict__ dq, int BH, int S, float qks, float sms) {
-  using C = I8BwdCfg<D>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nqb = (S + 127) / 128;
-  int bh, qt;
-  xcd_remap(blockIdx.x, nqb, BH, bh, qt);
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const int q0 = qt * 128 + wave * 32;
-  const bool active = q0 < S;
-  const long hrow = (long)bh * S;
-  const int nkt = S / 32;
-
-  auto stage = [&](int t, int buf) {
-    t = min(t, nkt - 1);
-    const long r0 = hrow + 32L * t;
-    char* base = smem + buf * C::B_STAGE;
-    for (int i = 0; i < C::B_IPW; ++i) {
-      int inst = wave + 4 * i;
-      constexpr int n8 = C::T8 / 1024;
-      if (inst < n8) {
-        dma_tile_inst<D, D, false>(reinterpret_cast<const char*>(ki + r0 * D), base, inst, lane);
-      } else if ((inst -= n8) < n8) {
-        dma_tile_inst<D, D, false>(reinterpret_cast<const char*>(vi + r0 * D), base + C::T8, inst, lane);
-      } else {
-        inst -= n8;
-        dma_tile_inst<D, 2 * D, true>(reinterpret_cast<const char*>(kb16 + r0 * D), base + 2 * C::T8,
-                                      inst, lane);
+      for (int i = 0; i < 16; ++i) {
+        const float P = exp2_f32(fmaf((float)sa[i], c1, -lsex));
+        X[i] = P * fmaf((float)pa[i], c2, -Dx);
       }
     }
   };
-  stage(0, 0);
-  stage(1, 1);
-  _Float16* sc_lds = reinterpret_cast<_Float16*>(smem + 3 * C::B_STAGE);
-  for (int i = tid; i < nkt; i += 256) {
-    sc_lds[i] = sk[hrow / 32 + i];
-    sc_lds[nkt + i] = sv[hrow / 32 + i];
-  }
-
-  v4i qfr[C::NKS8], ofr[C::NKS8];
-  float lq = 0.f, Dq = 0.f, sqw = 0.f, sdw = 0.f;
-  if (active) {
-    const long r = hrow + q0 + c32;
+  // per-tile quantisation of X into the two bf16 B operands
+  auto quantise = [&](int t, const float* X, v8bf* op) {
+    const float xmax = wave_max_dpp(ROLE == ROLE_DV ? max16_abs3(X) : max16_abs3(X));
+    const float sx = xmax * (1.0f / 127.0f);
+    const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
+    // DV: dO scale of the q tile; DK: q scale of the q tile; DQ: k scale of the k tile
+    const float so = (ROLE == ROLE_DV) ? (float)sc_lds[nt + t] : (float)sc_lds[t];
+    quant_operand(X, inv, sx * so, op);
+  };
+  auto tr_load = [&](int t, v8bf* ta) {
+    const char* base = slot(t);
 #pragma unroll
-    for (int s = 0; s < C::NKS8; ++s) {
-      qfr[s] = *reinterpret_cast<const v4i*>(qi + r * D + 16 * h + 32 * s);
-      ofr[s] = *reinterpret_cast<const v4i*>(dOi + r * D + 16 * h + 32 * s);
-    }
-    const float2 ldr = LD[r];
-    lq = ldr.x;
-    Dq = ldr.y;
-    sqw = (float)sq[(hrow + q0) / 32];
-    sdw = (float)sdO[(hrow + q0) / 32];
-  }
-  const float cq = sqw * qks;
-  v16f acc[C::NDB];
-#pragma unroll
-  for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
-  int roff[C::NKS8];
-#pragma unroll
-  for (int s = 0; s < C::NKS8; ++s) roff[s] = c32 * D + 16 * ((2 * s + h) ^ i8_sw<D>(c32));
-
-  vmem_drain();
-  vmcnt_wait<0>();
-  __syncthreads();
-  for (int t = 0; t < nkt; ++t) {
-    const int buf = t % 3;
-    stage(t + 2, (t + 2) % 3);
-    const char* base = smem + buf * C::B_STAGE;
-    const char* k8 = base;
-    const char* v8 = base + C::T8;
-    const char* kbl = base + 2 * C::T8;
-    const float skt = (float)sc_lds[t];
-    const float svt = (float)sc_lds[nkt + t];
-    if (active) {
-      v16i sacc = v16i{}, pacc = v16i{};
-#pragma unroll
-      for (int s = 0; s < C::NKS8; ++s) {
-        sacc = mfma_i8(*reinterpret_cast<const v4i*>(k8 + roff[s]), qfr[s], sacc);
-        pacc = mfma_i8(*reinterpret_cast<const v4i*>(v8 + roff[s]), ofr[s], pacc);
-      }
-      // same per-element operation order as kernel A:  ((acc*sq)*sk*qks) -> fma with -lse
-      const float c1 = sqw * (skt * qks), c2 = sdw * svt;
-      float dS[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float P = exp2_f32(fmaf((float)sacc[i], c1, -lq));
-        dS[i] = P * fmaf((float)pacc[i], c2, -Dq);
-      }
-      const float smax = wave_max_dpp(max16_abs(dS));
-      const float ssd = smax * (1.0f / 127.0f);
-      v8bf sb[2];
-      quant_operand(dS, ssd > 0.f ? 127.0f / smax : 0.f, ssd * skt, sb);
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) acc[b] = mfma_bf16(t16_frag<D>(kbl, 16 * s, b, lane), sb[s], acc[b]);
+        const char* a = base + troff[b] + 16 * s * 2 * D;
+        ta[s * C::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * 2 * D));
       }
-    }
-    vmcnt_wait<C::B_IPW>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+  };
+  auto accumulate = [&](const v8bf* ta, const v8bf* op) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < C::NDB; ++b) acc[b] = mfma_bf16(ta[s * C::NDB + b], op[s], acc[b]);
+  };
+
+  vmem_drain();
+  __syncthreads();
+  float X[16];
+  if (active) {
+    v16i sa, pa;
+    products(0, sa, pa);
+    values(0, sa, pa, X);
   }
-  vmcnt_wait<0>();
-  (void)cq;
+  for (int t = 0; t < nt; ++t) {
+    ring_wait_barrier<G::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
+    dma.issue(smem + ((t + 3) & 3) * G::SLOT, min(t + 3, nt - 1));
+    if (active) {
+      const int tn = min(t + 1, nt - 1);
+      v8bf ta[2 * C::NDB];
+      tr_load(t, ta);
+      v16i sa, pa;
+      products(tn, sa, pa);
+      v8bf op[2];
+      quantise(t, X, op);
+      accumulate(ta, op);
+      values(tn, sa, pa, X);
+    }
+  }
+  vmcnt_wait_all();
   if (!active) return;
-  const long r = hrow + q0 + c32;
+  const float osc = (ROLE == ROLE_DV) ? 1.0f : sms;
+  const long r = hrow + x0 + c32;
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       v4h w;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * sms);
-      *reinterpret_cast<v4h*>(dq + r * D + 32 * b + 8 * g + 4 * h) = w;
+      for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * osc);
+      *reinterpret_cast<v4h*>(out + r * D + 32 * b + 8 * g + 4 * h) = w;
     }
   }
 }
@@ -510,7 +426,45 @@ extern "C" int qattn_i8_to_bf16(const void* x, void* y, long n, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-// which: 1 = dK/dV kernel, 2 = dQ kernel, 3 = both
+template <int D, int ROLE>
+static void launch_bwd(const void* x8a, const void* x8b, const void* sxa, const void* sxb,
+                       const void* y8a, const void* y8b, const void* ytr, const void* yld,
+                       const void* sya, const void* syb, const void* xld, void* out, long bh,
+                       long seq, float qks, float sms, hipStream_t st) {
+  using G = BwdCfg<D, ROLE>;
+  const int lds = G::NSLOT * G::SLOT + (int)((2 * (seq / 32) * 2 + 15) / 16 * 16);
+  hipFuncSetAttribute((const void*)int8_bwd_kernel<D, ROLE>,
+                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  const int nb = (int)((seq + 127) / 128);
+  hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE>), dim3((unsigned)(nb * bh)), dim3(256), lds, st,
+                     (const int8_t*)x8a, (const int8_t*)x8b, (const _Float16*)sxa,
+                     (const _Float16*)sxb, (const int8_t*)y8a, (const int8_t*)y8b,
+                     (const __bf16*)ytr, (const float2*)yld, (const _Float16*)sya,
+                     (const _Float16*)syb, (const float2*)xld, (_Float16*)out, (int)bh, (int)seq,
+                     qks, sms);
+}
+
+// which: 1 = dV kernel, 4 = dK kernel, 2 = dQ kernel (bit mask)
+template <int D>
+static void bwd_launch_d(int which, const void* dO_i8, const void* sdO, const void* q_i8,
+                         const void* sq, const void* k_i8, const void* sk, const void* v_i8,
+                         const void* sv, const void* LD, const void* q_bf, const void* k_bf,
+                         const void* dO_bf, void* dq, void* dk, void* dv, long bh, long seq,
+                         float qks, float sms, hipStream_t st) {
+  // dV: own K (x8a) / streamed Q8 (y8a), dO image (ytr), LD; scales: sk|sv own, sq|sdO streamed
+  if (which & 1)
+    launch_bwd<D, ROLE_DV>(k_i8, nullptr, sk, sv, q_i8, nullptr, dO_bf, LD, sq, sdO, nullptr, dv, bh,
+                           seq, qks, sms, st);
+  // dK: own K, V / streamed Q8, dO8, q image, LD
+  if (which & 4)
+    launch_bwd<D, ROLE_DK>(k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, LD, sq, sdO, nullptr, dk, bh, seq,
+                           qks, sms, st);
+  // dQ: own Q, dO (+ their LD row stats) / streamed K8, V8, k image; scales: sq|sdO own, sk|sv
+  if (which & 2)
+    launch_bwd<D, ROLE_DQ>(q_i8, dO_i8, sq, sdO, k_i8, v_i8, k_bf, nullptr, sk, sv, LD, dq, bh, seq,
+                           qks, sms, st);
+}
+
 static int int8_bwd_launch(int which, const void* dO_i8, const void* sdO, const void* q_i8,
                            const void* sq, const void* k_i8, const void* sk, const void* v_i8,
                            const void* sv, const void* LD, const void* q_bf, const void* k_bf,
@@ -519,39 +473,12 @@ static int int8_bwd_launch(int which, const void* dO_i8, const void* sdO, const 
   if (seq % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
   if (bh == 0 || seq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int nb = (int)((seq + 127) / 128);
-#define QA_LAUNCH_A(Dv, M)                                                                       \
-  {                                                                                              \
-    const int sA = 3 * AStage<Dv, M>::BYTES + sc;                                                \
-    hipFuncSetAttribute((const void*)int8_bwd_dkdv_kernel<Dv, M>,                                \
-                        hipFuncAttributeMaxDynamicSharedMemorySize, sA);                         \
-    hipLaunchKernelGGL((int8_bwd_dkdv_kernel<Dv, M>), dim3((unsigned)(nb * bh)), dim3(256), sA,   \
-                       st, (const int8_t*)dO_i8, (const _Float16*)sdO, (const int8_t*)q_i8,       \
-                       (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,             \
-                       (const int8_t*)v_i8, (const _Float16*)sv, (const float2*)LD,               \
-                       (const __bf16*)q_bf, (const __bf16*)dO_bf, (_Float16*)dk, (_Float16*)dv,    \
-                       (int)bh, (int)seq, qks, sms);                                             \
-  }
-#define QA_LAUNCH(Dv)                                                                            \
-  {                                                                                              \
-    using C = I8BwdCfg<Dv>;                                                                      \
-    const int sc = (int)((2 * (seq / 32) * 2 + 15) / 16 * 16);                                   \
-    const int sB = 3 * C::B_STAGE + sc;                                                          \
-    if (which & 1) QA_LAUNCH_A(Dv, 1)                                                            \
-    if (which & 4) QA_LAUNCH_A(Dv, 2)                                                            \
-    if (which & 2) {                                                                             \
-      hipFuncSetAttribute((const void*)int8_bwd_dq_kernel<Dv>,                                   \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, sB);                       \
-      hipLaunchKernelGGL((int8_bwd_dq_kernel<Dv>), dim3((unsigned)(nb * bh)), dim3(256), sB, st,  \
-                         (const int8_t*)dO_i8, (const _Float16*)sdO, (const int8_t*)q_i8,         \
-                         (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,           \
-                         (const int8_t*)v_i8, (const _Float16*)sv, (const float2*)LD,             \
-                         (const __bf16*)k_bf, (_Float16*)dq, (int)bh, (int)seq, qks, sms);        \
-    }                                                                                            \
-  }
-  if (head_dim == 128) QA_LAUNCH(128) else QA_LAUNCH(64)
-#undef QA_LAUNCH
-#undef QA_LAUNCH_A
+  if (head_dim == 128)
+    bwd_launch_d<128>(which, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
+                      dv, bh, seq, qks, sms, st);
+  else
+    bwd_launch_d<64>(which, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
+                     dv, bh, seq, qks, sms, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
