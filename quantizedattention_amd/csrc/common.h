@@ -240,6 +240,36 @@ QA_DEVICE void ring_wait_barrier() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
+// ---------------------------------------------------------------- buffer LDS-DMA (ring staging)
+// buffer_load_dword{x4} ... offen lds: source = V#.base + voffset (lane-constant, swizzle applied)
+// + soffset (wave-uniform tile offset, SGPR); LDS destination = M0 + 16*lane (4*lane for dword).
+// Per piece only the M0 write and the load issue: no 64-bit per-lane address arithmetic.  M0 is
+// written without save/restore: the kernels that use these helpers contain no other M0 use
+// (tests/test_isa.py checks the disassembly), and the M0 -> LDS-DMA hazard takes one s_nop.
+QA_DEVICE v4u make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long a = (unsigned long)base;
+  v4u r;
+  r[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+  r[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32) & 0xffffu);   // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane(bytes);                            // range checked
+  r[3] = 0x00020000u;
+  return r;
+}
+QA_DEVICE unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)(p));
+}
+QA_DEVICE void dma16_buf(v4u rsrc, unsigned voff, unsigned soff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+               ::"v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+               : "memory");
+}
+QA_DEVICE void dma4_buf(v4u rsrc, unsigned voff, unsigned soff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
+               ::"v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+               : "memory");
+}
+
 // s_waitcnt vmcnt(0) as a real instruction hipcc's waitcnt pass understands: retire every ordinary
 // global load before a loop that issues asm LDS-DMA (otherwise the compiler's first-use wait for
 // those loads lands inside the loop and also waits for the in-flight DMA).

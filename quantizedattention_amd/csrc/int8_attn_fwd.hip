@@ -79,11 +79,12 @@ QA_DEVICE int v_sw(int row) {
 // LDS offset inside the slot and whether it reads V; the tile's base pointers are scalar.
 template <int D>
 struct DmaPlan {
-  unsigned voff[Int8FwdCfg<D>::IPW];
-  int lds_off[Int8FwdCfg<D>::IPW];
-  bool is_v[Int8FwdCfg<D>::IPW];
-  QA_DEVICE void init(int wave, int lane) {
-    using C = Int8FwdCfg<D>;
+  using C = Int8FwdCfg<D>;
+  unsigned voff[C::IPW];
+  unsigned lds_off[C::IPW];
+  unsigned stride[C::IPW];
+  v4u rsrc[C::IPW];
+  QA_DEVICE void init(int wave, int lane, int S, const int8_t* kbase, const _Float16* vbase) {
 #pragma unroll
     for (int i = 0; i < C::IPW; ++i) {
       int inst = wave + C::WAVES * i;
@@ -93,23 +94,23 @@ struct DmaPlan {
         const int row = inst * RPI + lane / C::K_CH, p = lane % C::K_CH;
         voff[i] = row * D + 16 * (p ^ k_sw<D>(row));
         lds_off[i] = inst * 1024;
-        is_v[i] = false;
+        stride[i] = C::K_BYTES;
+        rsrc[i] = make_rsrc(kbase, (unsigned)S * D);
       } else {
         const int vi = inst - C::K_INST;
         constexpr int RPI = 64 / C::V_CH;
         const int row = vi * RPI + lane / C::V_CH, p = lane % C::V_CH;
         voff[i] = row * 2 * D + 16 * (p ^ v_sw<D>(row));
         lds_off[i] = C::K_BYTES + vi * 1024;
-        is_v[i] = true;
+        stride[i] = C::V_BYTES;
+        rsrc[i] = make_rsrc(vbase, (unsigned)S * 2 * D);
       }
     }
   }
-  QA_DEVICE void issue(const int8_t* kbase, const _Float16* vbase, char* slot, int tile) const {
-    using C = Int8FwdCfg<D>;
-    const char* kb = reinterpret_cast<const char*>(kbase) + (long)tile * C::K_BYTES;
-    const char* vb = reinterpret_cast<const char*>(vbase) + (long)tile * C::V_BYTES;
+  QA_DEVICE void issue(unsigned slot_lds, int tile) const {
 #pragma unroll
-    for (int i = 0; i < C::IPW; ++i) glds16_s(is_v[i] ? vb : kb, voff[i], slot + lds_off[i]);
+    for (int i = 0; i < C::IPW; ++i)
+      dma16_buf(rsrc[i], voff[i], (unsigned)tile * stride[i], slot_lds + lds_off[i]);
   }
 };
 
@@ -153,11 +154,12 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
   const int nt = S / C::KT;
 
   DmaPlan<D> dma;
-  dma.init(wave, lane);
-  dma.issue(kbase, vbase, smem, 0);
+  dma.init(wave, lane, S, kbase, vbase);
+  const unsigned smem_lds = lds_addr(smem);
+  dma.issue(smem_lds, 0);
   if (STREAM) {
-    dma.issue(kbase, vbase, smem + 1 * C::SLOT, min(1, nt - 1));
-    dma.issue(kbase, vbase, smem + 2 * C::SLOT, min(2, nt - 1));
+    dma.issue(smem_lds + 1 * C::SLOT, min(1, nt - 1));
+    dma.issue(smem_lds + 2 * C::SLOT, min(2, nt - 1));
   }
   for (int i = tid; i < nt; i += 64 * C::WAVES) sk_lds[i] = sk[head_row0 / 32 + i];
 
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
 #else
       ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
 #endif
-      dma.issue(kbase, vbase, smem + ((t + 3) & 3) * C::SLOT, min(t + 3, nt - 1));
+      dma.issue(smem_lds + ((t + 3) & 3) * C::SLOT, min(t + 3, nt - 1));
     }
     if (active) {
       const int tn = min(t + 1, nt - 1);

@@ -129,10 +129,17 @@ struct BwdCfg {
   static constexpr int TR = TWO ? 2 * C::T8 : C::T8;
   static constexpr int LDO = TR + C::T16;
   static constexpr int SLOT = LDO + (HAS_LD ? 256 : 0);
-  static constexpr int NSLOT = 4;
+  // ring slots: 4 = two tiles of DMA latency cover; 3 = one tile, but 3 workgroups/CU fit in LDS
+#ifndef QA_BWD_NSLOT_DK
+#define QA_BWD_NSLOT_DK 4
+#endif
+  static constexpr int NSLOT = (ROLE == ROLE_DK) ? QA_BWD_NSLOT_DK : 4;
   static constexpr int NP8 = C::T8 / 1024, NP16 = C::T16 / 1024;
-  static constexpr int INST = NP8 * (TWO ? 2 : 1) + NP16 + (HAS_LD ? 1 : 0);
-  static constexpr int IPW = (INST + 3) / 4;
+  static constexpr int INST = NP8 * (TWO ? 2 : 1) + NP16;   // 1-KiB pieces per tile
+  static constexpr int IPW16 = (INST + 3) / 4;
+  // every wave also loads the tile's 256-B LD block (duplicate writes of the same bytes): one
+  // uniform instruction instead of a per-wave branch
+  static constexpr int IPW = IPW16 + (HAS_LD ? 1 : 0);      // VMEM ops per wave per tile
 };
 
 // LDS-DMA plan: per wave slot i (IPW of them) the region it fills (0 = Y8A, 1 = Y8B, 2 = TR, 3 = LD),
@@ -140,58 +147,48 @@ struct BwdCfg {
 template <int D, int ROLE>
 struct BwdDma {
   using G = BwdCfg<D, ROLE>;
-  unsigned voff[G::IPW];
-  int lds_off[G::IPW];
-  int reg[G::IPW];
-  const char* base[G::IPW];   // region tensor of the slot (head row 0) and its per-tile stride
-  int stride[G::IPW];
-  QA_DEVICE void init(int wave, int lane, const char* y8a, const char* y8b, const char* tr,
+  unsigned voff[G::IPW16];
+  unsigned lds_off[G::IPW16];
+  unsigned stride[G::IPW16];
+  v4u rsrc[G::IPW16];   // the slot's region tensor (head rows 0 .. S-1)
+  v4u ld_rsrc;
+  QA_DEVICE void init(int wave, int lane, int S, const char* y8a, const char* y8b, const char* tr,
                       const char* ld) {
 #pragma unroll
-    for (int i = 0; i < G::IPW; ++i) {
+    for (int i = 0; i < G::IPW16; ++i) {
       int p = wave + 4 * i;
       if (p >= G::INST) p = wave;   // padding slot: re-issue the wave's first piece (same bytes)
       if (p < G::NP8) {
-        set_i8(i, 0, G::Y8A, p, lane);
-        base[i] = y8a;
+        set_i8(i, G::Y8A, p, lane);
+        rsrc[i] = make_rsrc(y8a, (unsigned)S * D);
       } else if (G::TWO && p < 2 * G::NP8) {
-        set_i8(i, 1, G::Y8B, p - G::NP8, lane);
-        base[i] = y8b;
+        set_i8(i, G::Y8B, p - G::NP8, lane);
+        rsrc[i] = make_rsrc(y8b, (unsigned)S * D);
       } else {
         const int q = p - (G::TWO ? 2 : 1) * G::NP8;
-        if (q < G::NP16) {
-          constexpr int NCH = 2 * D / 16, RPI = 64 / NCH;
-          const int row = q * RPI + lane / NCH, c = lane % NCH;
-          voff[i] = row * 2 * D + 16 * (c ^ t16_sw<D>(row));
-          lds_off[i] = G::TR + q * 1024;
-          reg[i] = 2;
-          base[i] = tr;
-          stride[i] = 64 * D;
-        } else {
-          voff[i] = 4 * lane;
-          lds_off[i] = G::LDO;
-          reg[i] = 3;
-          base[i] = ld;
-          stride[i] = 256;
-        }
+        constexpr int NCH = 2 * D / 16, RPI = 64 / NCH;
+        const int row = q * RPI + lane / NCH, c = lane % NCH;
+        voff[i] = row * 2 * D + 16 * (c ^ t16_sw<D>(row));
+        lds_off[i] = G::TR + q * 1024;
+        stride[i] = 64 * D;
+        rsrc[i] = make_rsrc(tr, (unsigned)S * 2 * D);
       }
     }
+    if constexpr (G::HAS_LD) ld_rsrc = make_rsrc(ld, (unsigned)S * 8);
   }
-  QA_DEVICE void set_i8(int i, int r, int region, int piece, int lane) {
+  QA_DEVICE void set_i8(int i, int region, int piece, int lane) {
     constexpr int NCH = D / 16, RPI = 64 / NCH;
     const int row = piece * RPI + lane / NCH, c = lane % NCH;
     voff[i] = row * D + 16 * (c ^ i8_sw<D>(row));
     lds_off[i] = region + piece * 1024;
-    reg[i] = r;
     stride[i] = 32 * D;
   }
-  QA_DEVICE void issue(char* slot, int t) const {
+  // slot_lds: LDS byte address of the ring slot
+  QA_DEVICE void issue(unsigned slot_lds, int t, int lane) const {
 #pragma unroll
-    for (int i = 0; i < G::IPW; ++i) {
-      const char* b = base[i] + (long)t * stride[i];
-      if (reg[i] == 3) glds4_s(b, voff[i], slot + lds_off[i]);
-      else glds16_s(b, voff[i], slot + lds_off[i]);
-    }
+    for (int i = 0; i < G::IPW16; ++i)
+      dma16_buf(rsrc[i], voff[i], (unsigned)t * stride[i], slot_lds + lds_off[i]);
+    if constexpr (G::HAS_LD) dma4_buf(ld_rsrc, 4 * lane, (unsigned)t * 256, slot_lds + G::LDO);
   }
 };
 
@@ -230,10 +227,10 @@ __global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
   const char* gytr = reinterpret_cast<const char*>(ytr + hrow * D);
   const char* gyld = reinterpret_cast<const char*>(yld + hrow);
   BwdDma<D, ROLE> dma;
-  dma.init(wave, lane, gy8a, gy8b, gytr, gyld);
-  dma.issue(smem, 0);
-  dma.issue(smem + G::SLOT, min(1, nt - 1));
-  dma.issue(smem + 2 * G::SLOT, min(2, nt - 1));
+  dma.init(wave, lane, S, gy8a, gy8b, gytr, gyld);
+  const unsigned smem_lds = lds_addr(smem);
+#pragma unroll
+  for (int i = 0; i < G::NSLOT - 1; ++i) dma.issue(smem_lds + i * G::SLOT, min(i, nt - 1), lane);
   // per-tile scales of the streamed side, once, in LDS (a global load inside the loop would make
   // hipcc wait vmcnt for the in-flight LDS-DMA)
   _Float16* sc_lds = reinterpret_cast<_Float16*>(smem + G::NSLOT * G::SLOT);
@@ -277,7 +274,7 @@ __global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
 
-  auto slot = [&](int t) -> const char* { return smem + (t & 3) * G::SLOT; };
+  auto slot = [&](int t) -> const char* { return smem + (t % G::NSLOT) * G::SLOT; };
   // int8 products of tile t: S (and dP)
   auto products = [&](int t, v16i& sa, v16i& pa) {
     const char* base = slot(t);
@@ -360,8 +357,10 @@ __global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
     values(0, sa, pa, X);
   }
   for (int t = 0; t < nt; ++t) {
-    ring_wait_barrier<G::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
-    dma.issue(smem + ((t + 3) & 3) * G::SLOT, min(t + 3, nt - 1));
+    // tile t+1 landed (later tiles may be in flight); the slot of tile t-1 is free
+    ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
+    dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT, min(t + G::NSLOT - 1, nt - 1),
+              lane);
     if (active) {
       const int tn = min(t + 1, nt - 1);
       v8bf ta[2 * C::NDB];
