@@ -260,11 +260,15 @@ QA_DEVICE unsigned lds_addr(const void* p) {
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)(p));
 }
 QA_DEVICE void dma16_buf(v4u rsrc, unsigned voff, unsigned soff, unsigned lds) {
+  soff = __builtin_amdgcn_readfirstlane(soff);   // wave-uniform by construction; keep them in SGPRs
+  lds = __builtin_amdgcn_readfirstlane(lds);
   asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
                ::"v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
                : "memory");
 }
 QA_DEVICE void dma4_buf(v4u rsrc, unsigned voff, unsigned soff, unsigned lds) {
+  soff = __builtin_amdgcn_readfirstlane(soff);
+  lds = __builtin_amdgcn_readfirstlane(lds);
   asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
                ::"v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
                : "memory");

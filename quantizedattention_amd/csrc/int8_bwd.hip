@@ -371,6 +371,20 @@ __global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
       quantise(t, X, op);
       accumulate(ta, op);
       values(tn, sa, pa, X);
+#if defined(QA_BWD_SCHED)
+      // interleave: LDS reads first, then each MFMA followed by a bounded group of VALU
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * 2 * C::NDB + 2 * C::NKS8, 0);
+#pragma unroll
+      for (int i = 0; i < (TWO ? 2 : 1) * C::NKS8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, QA_BWD_SCHED, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 2 * C::NDB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, QA_BWD_SCHED2, 0);
+      }
+#endif
     }
   }
   vmcnt_wait_all();
