@@ -124,6 +124,10 @@ def int8_kernel_times(q, k, v, dO, n):
                                            P(LD), B * H, S, D, st),
         "i8_to_bf16_kernel(x3)": lambda: [_lib.call("qattn_i8_to_bf16", P(a), P(b), N * D, st)
                                           for a, b in ((qi, qb), (ki, kb), (dOi, ob))],
+        "int8_bwd_dkdv_kernel<dK+dV>": lambda: _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi),
+                                                         P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
+                                                         P(qb), P(ob), P(dk), P(dv), B * H, S, D,
+                                                         qks, sms, st),
         "int8_bwd_dkdv_kernel<dV>": lambda: _lib.call("qattn_int8_bwd_dv", P(dOi), P(sdO), P(qi), P(sq),
                                                   P(ki), P(sk), P(vi), P(sv), P(LD), P(qb), P(ob),
                                                   P(dk), P(dv), B * H, S, D, qks, sms, st),
@@ -222,8 +226,7 @@ def main():
     kt = int8_kernel_times(q, k, v, dO, max(3, a.steps // 2))
     per_call = {  # algorithmic MFMA work per launch
         "int8_attn_fwd_kernel": 4.0 * B * H * S * S * D,   # QK^T, PV
-        "int8_bwd_dkdv_kernel<dV>": 4.0 * B * H * S * S * D,   # S, dV
-        "int8_bwd_dkdv_kernel<dK>": 6.0 * B * H * S * S * D,   # S, dP, dK
+        "int8_bwd_dkdv_kernel<dK+dV>": 8.0 * B * H * S * S * D,   # S, dP, dV, dK (the step's kernel)
         "int8_bwd_dq_kernel": 6.0 * B * H * S * S * D,     # S, dP (recomputed), dQ
     }
     dom = max(per_call, key=lambda n: kt[n])

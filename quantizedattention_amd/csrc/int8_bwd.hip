@@ -103,47 +103,52 @@ __global__ __launch_bounds__(256) void i8_to_bf16_kernel(const int8_t* __restric
   reinterpret_cast<v4u*>(y)[2 * i + 1] = hi;
 }
 
-// ------------------------------------------------------------------ dV, dK, dQ: one kernel template
+// ------------------------------------------------------------ dV, dK, dQ: one kernel template
 // Every backward product has the same shape.  A wave owns 32 rows of one side X (keys for dV/dK,
 // queries for dQ) whose int8 fragments stay in registers, and streams 32-row tiles of the other
-// side Y through a 4-slot LDS ring (LDS-DMA, SADDR form, lane-constant swizzled source offsets):
-//   ROLE_DV: X = K           Y = {Q8, dO image, LD}      S          -> P  -> dV += dO^T P
-//   ROLE_DK: X = K, V        Y = {Q8, dO8, q image, LD}  S, dP      -> dS -> dK += q^T dS
-//   ROLE_DQ: X = Q, dO       Y = {K8, V8, k image}       S, dP      -> dS -> dQ += k^T dS^T
+// side Y through a 4-slot LDS ring (buffer LDS-DMA, lane-constant swizzled source offsets):
+//   ROLE_DV:  X = K     Y = {Q8, dO image, LD}                S     -> P      -> dV += dO^T P
+//   ROLE_DK:  X = K, V  Y = {Q8, dO8, q image, LD}            S, dP -> dS     -> dK += q^T dS
+//   ROLE_DKV: X = K, V  Y = {Q8, dO8, q image, dO image, LD}  S, dP -> P, dS  -> dK and dV
+//   ROLE_DQ:  X = Q, dO Y = {K8, V8, k image}                 S, dP -> dS     -> dQ += k^T dS^T
 // S and dP are int8 MFMAs (32x32x32) on the quantised operands; P = exp2(S*c1 - lse) and
-// dS = P*(dP*c2 - D) in fp32 (c1 = sq*(sk*qks), c2 = sdO*sv, identical in all three kernels so the
+// dS = P*(dP*c2 - D) in fp32 (c1 = sq*(sk*qks), c2 = sdO*sv, identical in all kernels so the
 // per-tile quantisation of P and dS is the same everywhere); P / dS are quantised per 32x32 tile
 // (amax/127, trunc, int8:363-365, 403-405) and enter a bf16 32x32x16 MFMA as the exact bf16 value
 // trunc(x/s) * s * s_other, against the exact bf16 image of the other int8 operand.
-// Software pipeline by one tile: the int8 MFMAs of tile t+1 are issued before the quantisation of
-// tile t, and the fp32 P/dS of tile t+1 are computed beside the bf16 MFMAs of tile t.
-enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2 };
+// PIPE: software pipeline by one tile (the int8 MFMAs of tile t+1 are issued before the
+// quantisation of tile t, the fp32 P/dS of tile t+1 are computed beside the bf16 MFMAs of tile t);
+// ROLE_DKV (two fp32 accumulators) runs unpipelined with 8 waves per workgroup instead.
+enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 
 template <int D, int ROLE>
 struct BwdCfg {
   using C = I8BwdCfg<D>;
-  static constexpr bool TWO = ROLE != ROLE_DV;     // S and dP (else S only)
-  static constexpr bool HAS_LD = ROLE != ROLE_DQ;  // per-row {lse, D} of the streamed side
+  static constexpr bool TWO = ROLE != ROLE_DV;              // S and dP (else S only)
+  static constexpr bool HAS_LD = ROLE != ROLE_DQ;           // per-row {lse, D} of the streamed side
+  static constexpr bool WANT_P = ROLE == ROLE_DV || ROLE == ROLE_DKV;
+  static constexpr bool WANT_DS = ROLE != ROLE_DV;
+  static constexpr int NTR = (ROLE == ROLE_DKV) ? 2 : 1;    // transposed images per tile
+  static constexpr int WAVES = (ROLE == ROLE_DKV) ? 8 : 4;
+  static constexpr bool PIPE = ROLE != ROLE_DKV;
   static constexpr int Y8A = 0;
   static constexpr int Y8B = C::T8;
-  static constexpr int TR = TWO ? 2 * C::T8 : C::T8;
-  static constexpr int LDO = TR + C::T16;
+  static constexpr int TR = TWO ? 2 * C::T8 : C::T8;        // image of the dS product (or P for DV)
+  static constexpr int TR2 = TR + C::T16;                   // DKV: dO image (P product)
+  static constexpr int LDO = TR + NTR * C::T16;
   static constexpr int SLOT = LDO + (HAS_LD ? 256 : 0);
-  // ring slots: 4 = two tiles of DMA latency cover; 3 = one tile, but 3 workgroups/CU fit in LDS
-#ifndef QA_BWD_NSLOT_DK
-#define QA_BWD_NSLOT_DK 4
-#endif
-  static constexpr int NSLOT = (ROLE == ROLE_DK) ? QA_BWD_NSLOT_DK : 4;
+  static constexpr int NSLOT = 4;
   static constexpr int NP8 = C::T8 / 1024, NP16 = C::T16 / 1024;
-  static constexpr int INST = NP8 * (TWO ? 2 : 1) + NP16;   // 1-KiB pieces per tile
-  static constexpr int IPW16 = (INST + 3) / 4;
+  static constexpr int INST = NP8 * (TWO ? 2 : 1) + NTR * NP16;   // 1-KiB pieces per tile
+  static constexpr int IPW16 = (INST + WAVES - 1) / WAVES;
   // every wave also loads the tile's 256-B LD block (duplicate writes of the same bytes): one
   // uniform instruction instead of a per-wave branch
   static constexpr int IPW = IPW16 + (HAS_LD ? 1 : 0);      // VMEM ops per wave per tile
+  static constexpr int XROWS = 32 * WAVES;                  // own rows per workgroup
 };
 
-// LDS-DMA plan: per wave slot i (IPW of them) the region it fills (0 = Y8A, 1 = Y8B, 2 = TR, 3 = LD),
-// its lane-constant source byte offset inside the region's tile and its LDS offset inside the slot.
+// LDS-DMA plan: per wave slot i the lane-constant source byte offset inside the region's tile, the
+// LDS offset inside the ring slot, the region's per-tile stride and its buffer descriptor.
 template <int D, int ROLE>
 struct BwdDma {
   using G = BwdCfg<D, ROLE>;
@@ -153,10 +158,10 @@ struct BwdDma {
   v4u rsrc[G::IPW16];   // the slot's region tensor (head rows 0 .. S-1)
   v4u ld_rsrc;
   QA_DEVICE void init(int wave, int lane, int S, const char* y8a, const char* y8b, const char* tr,
-                      const char* ld) {
+                      const char* tr2, const char* ld) {
 #pragma unroll
     for (int i = 0; i < G::IPW16; ++i) {
-      int p = wave + 4 * i;
+      int p = wave + G::WAVES * i;
       if (p >= G::INST) p = wave;   // padding slot: re-issue the wave's first piece (same bytes)
       if (p < G::NP8) {
         set_i8(i, G::Y8A, p, lane);
@@ -165,13 +170,15 @@ struct BwdDma {
         set_i8(i, G::Y8B, p - G::NP8, lane);
         rsrc[i] = make_rsrc(y8b, (unsigned)S * D);
       } else {
-        const int q = p - (G::TWO ? 2 : 1) * G::NP8;
+        int q = p - (G::TWO ? 2 : 1) * G::NP8;
+        const bool second = q >= G::NP16;
+        if (second) q -= G::NP16;
         constexpr int NCH = 2 * D / 16, RPI = 64 / NCH;
         const int row = q * RPI + lane / NCH, c = lane % NCH;
         voff[i] = row * 2 * D + 16 * (c ^ t16_sw<D>(row));
-        lds_off[i] = G::TR + q * 1024;
+        lds_off[i] = (second ? G::TR2 : G::TR) + q * 1024;
         stride[i] = 64 * D;
-        rsrc[i] = make_rsrc(tr, (unsigned)S * 2 * D);
+        rsrc[i] = make_rsrc(second ? tr2 : tr, (unsigned)S * 2 * D);
       }
     }
     if constexpr (G::HAS_LD) ld_rsrc = make_rsrc(ld, (unsigned)S * 8);
@@ -201,40 +208,40 @@ QA_DEVICE float max16_abs3(const float* x) {
 }
 
 template <int D, int ROLE>
-__global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
+__global__ __launch_bounds__((64 * BwdCfg<D, ROLE>::WAVES), (8 / BwdCfg<D, ROLE>::WAVES))
+void int8_bwd_kernel(
     const int8_t* __restrict__ x8a, const int8_t* __restrict__ x8b, const _Float16* __restrict__ sxa,
     const _Float16* __restrict__ sxb, const int8_t* __restrict__ y8a, const int8_t* __restrict__ y8b,
-    const __bf16* __restrict__ ytr, const float2* __restrict__ yld, const _Float16* __restrict__ sya,
-    const _Float16* __restrict__ syb, const float2* __restrict__ xld, _Float16* __restrict__ out,
-    int BH, int S, float qks, float sms) {
+    const __bf16* __restrict__ ytr, const __bf16* __restrict__ ytr2, const float2* __restrict__ yld,
+    const _Float16* __restrict__ sya, const _Float16* __restrict__ syb,
+    const float2* __restrict__ xld, _Float16* __restrict__ out, _Float16* __restrict__ out2, int BH,
+    int S, float qks, float sms) {
   using C = I8BwdCfg<D>;
   using G = BwdCfg<D, ROLE>;
   constexpr bool TWO = G::TWO;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nxb = (S + 127) / 128;
+  const int nxb = (S + G::XROWS - 1) / G::XROWS;
   int bh, xt;
   xcd_remap(blockIdx.x, nxb, BH, bh, xt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const int x0 = xt * 128 + wave * 32;
+  const int x0 = xt * G::XROWS + wave * 32;
   const bool active = x0 < S;
   const long hrow = (long)bh * S;
   const int nt = S / 32;
 
-  const char* gy8a = reinterpret_cast<const char*>(y8a + hrow * D);
-  const char* gy8b = reinterpret_cast<const char*>(y8b + hrow * D);
-  const char* gytr = reinterpret_cast<const char*>(ytr + hrow * D);
-  const char* gyld = reinterpret_cast<const char*>(yld + hrow);
   BwdDma<D, ROLE> dma;
-  dma.init(wave, lane, S, gy8a, gy8b, gytr, gyld);
+  dma.init(wave, lane, S, reinterpret_cast<const char*>(y8a + hrow * D),
+           reinterpret_cast<const char*>(y8b + hrow * D), reinterpret_cast<const char*>(ytr + hrow * D),
+           reinterpret_cast<const char*>(ytr2 + hrow * D), reinterpret_cast<const char*>(yld + hrow));
   const unsigned smem_lds = lds_addr(smem);
 #pragma unroll
   for (int i = 0; i < G::NSLOT - 1; ++i) dma.issue(smem_lds + i * G::SLOT, min(i, nt - 1), lane);
   // per-tile scales of the streamed side, once, in LDS (a global load inside the loop would make
   // hipcc wait vmcnt for the in-flight LDS-DMA)
   _Float16* sc_lds = reinterpret_cast<_Float16*>(smem + G::NSLOT * G::SLOT);
-  for (int i = tid; i < nt; i += 256) {
+  for (int i = tid; i < nt; i += 64 * G::WAVES) {
     sc_lds[i] = sya[hrow / 32 + i];
     sc_lds[nt + i] = syb[hrow / 32 + i];
   }
@@ -267,12 +274,16 @@ __global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
 #pragma unroll
     for (int b = 0; b < C::NDB; ++b) {
       const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
-      troff[b] = G::TR + row * 2 * D + 16 * ((d / 8) ^ t16_sw<D>(row)) + (d % 8) * 2;
+      troff[b] = row * 2 * D + 16 * ((d / 8) ^ t16_sw<D>(row)) + (d % 8) * 2;
     }
   }
-  v16f acc[C::NDB];
+  v16f acc[C::NDB], acc2[ROLE == ROLE_DKV ? C::NDB : 1];
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
+  if constexpr (ROLE == ROLE_DKV) {
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) acc2[b] = v16f{};
+  }
 
   auto slot = [&](int t) -> const char* { return smem + (t % G::NSLOT) * G::SLOT; };
   // int8 products of tile t: S (and dP)
@@ -286,8 +297,8 @@ __global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
       if constexpr (TWO) pa = mfma_i8(*reinterpret_cast<const v4i*>(base + G::Y8B + roff[s]), xb[s], pa);
     }
   };
-  // fp32 P (DV) or dS (DK, DQ) of tile t
-  auto values = [&](int t, const v16i& sa, const v16i& pa, float* X) {
+  // fp32 P and/or dS of tile t
+  auto values = [&](int t, const v16i& sa, const v16i& pa, float* P, float* dS) {
     // c1 = sq*(sk*qks), c2 = sdO*sv with the streamed / own roles of each kernel
     const float sy_a = (float)sc_lds[t], sy_b = (float)sc_lds[nt + t];
     float c1, c2;
@@ -309,30 +320,29 @@ __global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
-          const float P = exp2_f32(fmaf((float)sa[i], c1, -lse_r[j]));
-          if constexpr (TWO) X[i] = P * fmaf((float)pa[i], c2, -d_r[j]);
-          else X[i] = P;
+          const float p = exp2_f32(fmaf((float)sa[i], c1, -lse_r[j]));
+          if constexpr (G::WANT_P) P[i] = p;
+          if constexpr (G::WANT_DS) dS[i] = p * fmaf((float)pa[i], c2, -d_r[j]);
         }
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float P = exp2_f32(fmaf((float)sa[i], c1, -lsex));
-        X[i] = P * fmaf((float)pa[i], c2, -Dx);
+        const float p = exp2_f32(fmaf((float)sa[i], c1, -lsex));
+        dS[i] = p * fmaf((float)pa[i], c2, -Dx);
       }
     }
   };
-  // per-tile quantisation of X into the two bf16 B operands
-  auto quantise = [&](int t, const float* X, v8bf* op) {
-    const float xmax = wave_max_dpp(ROLE == ROLE_DV ? max16_abs3(X) : max16_abs3(X));
+  // per-tile quantisation of X into the two bf16 B operands, scaled by so (the other operand's
+  // per-tile scale)
+  auto quantise = [&](const float* X, float so, v8bf* op) {
+    const float xmax = wave_max_dpp(max16_abs3(X));
     const float sx = xmax * (1.0f / 127.0f);
     const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
-    // DV: dO scale of the q tile; DK: q scale of the q tile; DQ: k scale of the k tile
-    const float so = (ROLE == ROLE_DV) ? (float)sc_lds[nt + t] : (float)sc_lds[t];
     quant_operand(X, inv, sx * so, op);
   };
-  auto tr_load = [&](int t, v8bf* ta) {
-    const char* base = slot(t);
+  auto tr_load = [&](int t, int region, v8bf* ta) {
+    const char* base = slot(t) + region;
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -341,66 +351,82 @@ __global__ __launch_bounds__(256, 2) void int8_bwd_kernel(
         ta[s * C::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * 2 * D));
       }
   };
-  auto accumulate = [&](const v8bf* ta, const v8bf* op) {
+  auto accumulate = [&](v16f* ac, const v8bf* ta, const v8bf* op) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int b = 0; b < C::NDB; ++b) acc[b] = mfma_bf16(ta[s * C::NDB + b], op[s], acc[b]);
+      for (int b = 0; b < C::NDB; ++b) ac[b] = mfma_bf16(ta[s * C::NDB + b], op[s], ac[b]);
   };
+  // scale of the other operand of the accumulating product: DV/DKV-P: dO of the q tile (syb);
+  // DK/DKV-dS: q of the q tile (sya); DQ: k of the k tile (sya)
+  auto so_p = [&](int t) { return (float)sc_lds[nt + t]; };
+  auto so_ds = [&](int t) { return (float)sc_lds[t]; };
 
   vmem_drain();
   __syncthreads();
-  float X[16];
-  if (active) {
-    v16i sa, pa;
-    products(0, sa, pa);
-    values(0, sa, pa, X);
-  }
-  for (int t = 0; t < nt; ++t) {
-    // tile t+1 landed (later tiles may be in flight); the slot of tile t-1 is free
-    ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
-    dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT, min(t + G::NSLOT - 1, nt - 1),
-              lane);
+  if constexpr (G::PIPE) {
+    float X[16];
     if (active) {
-      const int tn = min(t + 1, nt - 1);
-      v8bf ta[2 * C::NDB];
-      tr_load(t, ta);
       v16i sa, pa;
-      products(tn, sa, pa);
-      v8bf op[2];
-      quantise(t, X, op);
-      accumulate(ta, op);
-      values(tn, sa, pa, X);
-#if defined(QA_BWD_SCHED)
-      // interleave: LDS reads first, then each MFMA followed by a bounded group of VALU
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * 2 * C::NDB + 2 * C::NKS8, 0);
-#pragma unroll
-      for (int i = 0; i < (TWO ? 2 : 1) * C::NKS8; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, QA_BWD_SCHED, 0);
+      products(0, sa, pa);
+      values(0, sa, pa, X, X);
+    }
+    for (int t = 0; t < nt; ++t) {
+      // tile t+1 landed (later tiles may be in flight); the slot of tile t-1 is free
+      ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
+      dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
+                min(t + G::NSLOT - 1, nt - 1), lane);
+      if (active) {
+        const int tn = min(t + 1, nt - 1);
+        v8bf ta[2 * C::NDB];
+        tr_load(t, G::TR, ta);
+        v16i sa, pa;
+        products(tn, sa, pa);
+        v8bf op[2];
+        quantise(X, ROLE == ROLE_DV ? so_p(t) : so_ds(t), op);
+        accumulate(acc, ta, op);
+        values(tn, sa, pa, X, X);
       }
-#pragma unroll
-      for (int i = 0; i < 2 * C::NDB; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, QA_BWD_SCHED2, 0);
+    }
+  } else {
+    for (int t = 0; t < nt; ++t) {
+      // tile t landed (t+1, t+2 may be in flight); the slot of tile t-1 is free
+      ring_wait_barrier<(G::NSLOT - 2) * G::IPW>();
+      dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
+                min(t + G::NSLOT - 1, nt - 1), lane);
+      if (active) {
+        v16i sa, pa;
+        products(t, sa, pa);
+        float P[16], dS[16];
+        values(t, sa, pa, P, dS);
+        v8bf opS[2], opP[2];
+        quantise(dS, so_ds(t), opS);
+        quantise(P, so_p(t), opP);
+        v8bf ta[2 * C::NDB];
+        tr_load(t, G::TR, ta);
+        accumulate(acc, ta, opS);          // dK += q^T dS
+        tr_load(t, G::TR2, ta);
+        accumulate(acc2, ta, opP);         // dV += dO^T P
       }
-#endif
     }
   }
   vmcnt_wait_all();
   if (!active) return;
-  const float osc = (ROLE == ROLE_DV) ? 1.0f : sms;
   const long r = hrow + x0 + c32;
+  auto store = [&](const v16f* ac, float osc, _Float16* dst) {
 #pragma unroll
-  for (int b = 0; b < C::NDB; ++b) {
+    for (int b = 0; b < C::NDB; ++b) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      v4h w;
+      for (int g = 0; g < 4; ++g) {
+        v4h w;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * osc);
-      *reinterpret_cast<v4h*>(out + r * D + 32 * b + 8 * g + 4 * h) = w;
+        for (int j = 0; j < 4; ++j) w[j] = (_Float16)(ac[b][4 * g + j] * osc);
+        *reinterpret_cast<v4h*>(dst + r * D + 32 * b + 8 * g + 4 * h) = w;
+      }
     }
-  }
+  };
+  store(acc, ROLE == ROLE_DV ? 1.0f : sms, out);
+  if constexpr (ROLE == ROLE_DKV) store(acc2, 1.0f, out2);
 }
 
 }  // namespace qattn
@@ -441,23 +467,23 @@ extern "C" int qattn_i8_to_bf16(const void* x, void* y, long n, void* stream) {
 
 template <int D, int ROLE>
 static void launch_bwd(const void* x8a, const void* x8b, const void* sxa, const void* sxb,
-                       const void* y8a, const void* y8b, const void* ytr, const void* yld,
-                       const void* sya, const void* syb, const void* xld, void* out, long bh,
-                       long seq, float qks, float sms, hipStream_t st) {
+                       const void* y8a, const void* y8b, const void* ytr, const void* ytr2,
+                       const void* yld, const void* sya, const void* syb, const void* xld, void* out,
+                       void* out2, long bh, long seq, float qks, float sms, hipStream_t st) {
   using G = BwdCfg<D, ROLE>;
   const int lds = G::NSLOT * G::SLOT + (int)((2 * (seq / 32) * 2 + 15) / 16 * 16);
   hipFuncSetAttribute((const void*)int8_bwd_kernel<D, ROLE>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  const int nb = (int)((seq + 127) / 128);
-  hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE>), dim3((unsigned)(nb * bh)), dim3(256), lds, st,
-                     (const int8_t*)x8a, (const int8_t*)x8b, (const _Float16*)sxa,
+  const int nb = (int)((seq + G::XROWS - 1) / G::XROWS);
+  hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES), lds,
+                     st, (const int8_t*)x8a, (const int8_t*)x8b, (const _Float16*)sxa,
                      (const _Float16*)sxb, (const int8_t*)y8a, (const int8_t*)y8b,
-                     (const __bf16*)ytr, (const float2*)yld, (const _Float16*)sya,
-                     (const _Float16*)syb, (const float2*)xld, (_Float16*)out, (int)bh, (int)seq,
-                     qks, sms);
+                     (const __bf16*)ytr, (const __bf16*)ytr2, (const float2*)yld,
+                     (const _Float16*)sya, (const _Float16*)syb, (const float2*)xld,
+                     (_Float16*)out, (_Float16*)out2, (int)bh, (int)seq, qks, sms);
 }
 
-// which: 1 = dV kernel, 4 = dK kernel, 2 = dQ kernel (bit mask)
+// which: bit mask 1 = dV kernel, 4 = dK kernel, 8 = fused dK+dV kernel, 2 = dQ kernel
 template <int D>
 static void bwd_launch_d(int which, const void* dO_i8, const void* sdO, const void* q_i8,
                          const void* sq, const void* k_i8, const void* sk, const void* v_i8,
@@ -466,16 +492,20 @@ static void bwd_launch_d(int which, const void* dO_i8, const void* sdO, const vo
                          float qks, float sms, hipStream_t st) {
   // dV: own K (x8a) / streamed Q8 (y8a), dO image (ytr), LD; scales: sk|sv own, sq|sdO streamed
   if (which & 1)
-    launch_bwd<D, ROLE_DV>(k_i8, nullptr, sk, sv, q_i8, nullptr, dO_bf, LD, sq, sdO, nullptr, dv, bh,
-                           seq, qks, sms, st);
+    launch_bwd<D, ROLE_DV>(k_i8, nullptr, sk, sv, q_i8, nullptr, dO_bf, nullptr, LD, sq, sdO, nullptr,
+                           dv, nullptr, bh, seq, qks, sms, st);
   // dK: own K, V / streamed Q8, dO8, q image, LD
   if (which & 4)
-    launch_bwd<D, ROLE_DK>(k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, LD, sq, sdO, nullptr, dk, bh, seq,
-                           qks, sms, st);
+    launch_bwd<D, ROLE_DK>(k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, nullptr, LD, sq, sdO, nullptr, dk,
+                           nullptr, bh, seq, qks, sms, st);
+  // dK and dV in one pass: + dO image
+  if (which & 8)
+    launch_bwd<D, ROLE_DKV>(k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, dO_bf, LD, sq, sdO, nullptr, dk,
+                            dv, bh, seq, qks, sms, st);
   // dQ: own Q, dO (+ their LD row stats) / streamed K8, V8, k image; scales: sq|sdO own, sk|sv
   if (which & 2)
-    launch_bwd<D, ROLE_DQ>(q_i8, dO_i8, sq, sdO, k_i8, v_i8, k_bf, nullptr, sk, sv, LD, dq, bh, seq,
-                           qks, sms, st);
+    launch_bwd<D, ROLE_DQ>(q_i8, dO_i8, sq, sdO, k_i8, v_i8, k_bf, nullptr, nullptr, sk, sv, LD, dq,
+                           nullptr, bh, seq, qks, sms, st);
 }
 
 static int int8_bwd_launch(int which, const void* dO_i8, const void* sdO, const void* q_i8,
@@ -500,7 +530,7 @@ extern "C" int qattn_int8_attn_bwd(const void* dO_i8, const void* sdO, const voi
                                    const void* sv, const void* LD, const void* q_bf, const void* k_bf,
                                    const void* dO_bf, void* dq, void* dk, void* dv, long bh, long seq,
                                    int head_dim, float qks, float sms, void* stream) {
-  return int8_bwd_launch(7, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
+  return int8_bwd_launch(8 | 2, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
                          dv, bh, seq, head_dim, qks, sms, stream);
 }
 extern "C" int qattn_int8_bwd_dkdv(const void* dO_i8, const void* sdO, const void* q_i8,
@@ -508,7 +538,7 @@ extern "C" int qattn_int8_bwd_dkdv(const void* dO_i8, const void* sdO, const voi
                                    const void* sv, const void* LD, const void* q_bf, const void* dO_bf,
                                    void* dk, void* dv, long bh, long seq, int head_dim, float qks,
                                    float sms, void* stream) {
-  return int8_bwd_launch(5, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, nullptr, dO_bf,
+  return int8_bwd_launch(8, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, nullptr, dO_bf,
                          nullptr, dk, dv, bh, seq, head_dim, qks, sms, stream);
 }
 extern "C" int qattn_int8_bwd_dv(const void* dO_i8, const void* sdO, const void* q_i8,

@@ -17,7 +17,7 @@ from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp
 
 name = sys.argv[1]
 if name == "int8_all":  # every int8 attention kernel once per rep, in step order
-    names = ["int8_fwd", "int8_dv", "int8_dk", "int8_dq"]
+    names = ["int8_fwd", "int8_dkdv", "int8_dq"]
 else:
     names = [name]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
