@@ -289,8 +289,11 @@ void int8_bwd_kernel(
   // int8 products of tile t: S (and dP)
   auto products = [&](int t, v16i& sa, v16i& pa) {
     const char* base = slot(t);
-    sa = v16i{};
-    pa = v16i{};
+    // DQ: accumulators start at the bit pattern of 1.5*2^23, so the int32 result read as fp32 is
+    // exactly 1.5*2^23 + acc (|acc| < 2^22): no int->float conversion per score (see values())
+    constexpr int bias = (ROLE == ROLE_DQ) ? 0x4B400000 : 0;
+    sa = v16i{} + bias;
+    pa = v16i{} + bias;
 #pragma unroll
     for (int s = 0; s < C::NKS8; ++s) {
       sa = mfma_i8(*reinterpret_cast<const v4i*>(base + G::Y8A + roff[s]), xa[s], sa);
@@ -326,10 +329,14 @@ void int8_bwd_kernel(
         }
       }
     } else {
+      // per-lane row stats: fold the 1.5*2^23 accumulator bias into the constants (one rounding of
+      // the constant, well below the int8 quantisation noise)
+      constexpr float M = 12582912.0f;
+      const float k1 = -fmaf(c1, M, lsex), k2 = -fmaf(c2, M, Dx);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2_f32(fmaf((float)sa[i], c1, -lsex));
-        dS[i] = p * fmaf((float)pa[i], c2, -Dx);
+        const float p = exp2_f32(fmaf(__int_as_float(sa[i]), c1, k1));
+        dS[i] = p * fmaf(__int_as_float(pa[i]), c2, k2);
       }
     }
   };
