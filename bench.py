@@ -31,8 +31,7 @@ sys.path.insert(0, ROOT)
 from quantizedattention_amd import _lib  # noqa: E402
 from quantizedattention_amd.attention_bf16 import (  # noqa: E402
     helion_atten_bf16_fwd_training, helion_flash_atten_2_algo_4_bwd)
-from quantizedattention_amd.attention_int8 import (  # noqa: E402
-    _int8_forward, helion_atten_int8_hl_dot_bwd)
+from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward  # noqa: E402
 
 PEAK_I8 = 256 * 8192 * 2.4e9          # ops/s, dense int8 MFMA (MI355X_MICROARCH: 2x bf16 per clock)
 PEAK_BF16 = 256 * 4096 * 2.4e9        # flop/s, dense bf16/fp16 MFMA
@@ -112,18 +111,16 @@ def int8_kernel_times(q, k, v, dO, n):
     qks, sms = _f32(1 / math.sqrt(D) * 1.44269504), _f32(1 / math.sqrt(D))
     calls = {
         "kmean_kernel": lambda: _lib.call("qattn_kmean", P(k), P(km), B * H, S, D, st),
-        "quant_block32_kernel(k)": lambda: _lib.call("qattn_int8_quant", P(k), P(ki), P(sk), None,
-                                                     P(km), N, S, D, st),
-        "quant_block32_kernel(q)": lambda: _lib.call("qattn_int8_quant", P(q), P(qi), P(sq), None,
-                                                     None, N, S, D, st),
+        "quant_block32_kernel(k)": lambda: _lib.call("qattn_int8_quant_img", P(k), P(ki), P(sk), None,
+                                                     P(kb), P(km), N, S, D, st),
+        "quant_block32_kernel(q)": lambda: _lib.call("qattn_int8_quant_img", P(q), P(qi), P(sq), None,
+                                                     P(qb), None, N, S, D, st),
         "quant_block32_kernel(v)": lambda: _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq),
                                                      None, N, S, D, st),
         "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk),
                                                   P(vdq), P(O), P(lse), B * H, S, D, qks, st),
         "int8_bwd_prep": lambda: _lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(lse), P(dOi), P(sdO),
-                                           P(LD), B * H, S, D, st),
-        "i8_to_bf16_kernel(x3)": lambda: [_lib.call("qattn_i8_to_bf16", P(a), P(b), N * D, st)
-                                          for a, b in ((qi, qb), (ki, kb), (dOi, ob))],
+                                           P(LD), P(ob), B * H, S, D, st),
         "int8_bwd_dkdv_kernel<dK+dV>": lambda: _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi),
                                                          P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
                                                          P(qb), P(ob), P(dk), P(dv), B * H, S, D,
@@ -184,13 +181,14 @@ def main():
     comm = torch.cuda.Stream(device=dev) if gather else None
 
     def step_int8():
-        O, lse, qi, kiT, vi, sq, sk, sv, km = _int8_forward(q, k, v, smooth=True)
+        # the autograd path of sage_attention_3_int8: quantiser passes also write the bf16 images
+        O, lse, qi, kiT, vi, sq, sk, sv, km, qb_, kb_ = _int8_forward(q, k, v, smooth=True, images=True)
         work = None
         if gather:
             comm.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(comm):
                 work = dist.all_gather_into_tensor(O_full, O.view(B * H, S, D), async_op=True)
-        helion_atten_int8_hl_dot_bwd(dO, qi, sq, kiT, km, sk, vi, sv, O, lse, 32, 32)
+        _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb_, kb_)
         if work is not None:
             work.wait()
             torch.cuda.current_stream().wait_stream(comm)

@@ -40,6 +40,11 @@ extern "C" {
  * Bit-exact with the reference's eager-torch rounding.  rows % 32 == 0. */
 int qattn_int8_quant(const void* x, void* idx, void* scale, void* deq, const void* kmean, long rows,
                      int rows_per_head, int head_dim, void* stream);
+/* Same, with an optional exact bf16 image of idx (img bf16 [rows, D], or NULL): the backward's
+ * transposed-read operand for q and k, written in the same pass.  deq and img are exclusive. */
+int qattn_int8_quant_img(const void* x, void* idx, void* scale, void* deq, void* img,
+                         const void* kmean, long rows, int rows_per_head, int head_dim,
+                         void* stream);
 
 /* k_mean = f16(mean over the S tokens of each head) — k f16 [bh*seq, D] -> kmean f16 [bh, D]
  * (SageAttention smoothing; replaces the crashing `k.mean(0)` of attention_int8.py:24-25). */
@@ -53,10 +58,11 @@ int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, cons
                         const void* vdq, void* out, void* lse, long bh, long seq, int head_dim,
                         float qks, void* stream);
 
-/* Backward prologue (attention_int8.py:372-374, 398): dO f16 -> dO_i8 [rows, D] + sdO f16 [rows/32]
- * (same quantiser), and LD f32x2 [rows] = {f32(lse), f32(f16(rowsum(dO*O)))}. */
+/* Backward prologue, one pass (attention_int8.py:372-374, 398): dO f16 -> dO_i8 [rows, D] + sdO f16
+ * [rows/32] (same quantiser), dO_bf = bf16(dO_i8) [rows, D] (optional, NULL to skip), and LD f32x2
+ * [rows] = {f32(lse), f32(f16(rowsum(dO*O)))}. */
 int qattn_int8_bwd_prep(const void* dO, const void* O, const void* lse, void* dO_i8, void* sdO,
-                        void* LD, long bh, long seq, int head_dim, void* stream);
+                        void* LD, void* dO_bf, long bh, long seq, int head_dim, void* stream);
 
 /* Exact widening copy i8 -> bf16 of n elements (n % 16 == 0): the transposed-read operand images
  * of q_i8, k_i8, dO_i8 used by the dK / dQ / dV products (no reference counterpart). */

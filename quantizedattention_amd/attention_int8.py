@@ -50,7 +50,13 @@ def _check_shapes(q, k, v):
         raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
 
 
-def _int8_forward(q, k, v, smooth: bool):
+def _int8_forward(q, k, v, smooth: bool, images: bool = False):
+    """Quantise q, k, v and run the int8 attention forward.
+
+    Returns (O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean, q_bf, k_bf); q_bf / k_bf are the exact
+    bf16 images of q_i8 / k_i8 the backward reads (written by the same quantiser pass when
+    ``images``, else None).
+    """
     _check_shapes(q, k, v)
     _lib.require_gpu(q, k, v)
     q = q.to(torch.float16).contiguous()
@@ -69,12 +75,17 @@ def _int8_forward(q, k, v, smooth: bool):
     vdq = torch.empty((N, D), dtype=torch.float16, device=dev)  # workspace fp16(v_i8 * sv)
     O = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
     lse = torch.empty((N,), dtype=torch.float16, device=dev)
+    q_bf = k_bf = None
+    if images:
+        q_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
+        k_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
     k_mean = None
     if smooth:
         k_mean = torch.empty((B, H, 1, D), dtype=torch.float16, device=dev)
         _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(k_mean), B * H, S, D, st)
-    _lib.call("qattn_int8_quant", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), None, None, N, S, D, st)
-    _lib.call("qattn_int8_quant", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None,
+    _lib.call("qattn_int8_quant_img", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), None, _lib.ptr(q_bf),
+              None, N, S, D, st)
+    _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
               _lib.ptr(k_mean), N, S, D, st)
     _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vdq), None,
               N, S, D, st)
@@ -83,7 +94,46 @@ def _int8_forward(q, k, v, smooth: bool):
               float(torch.tensor(_qk_scale(D), dtype=torch.float32)), st)
     # k_i8T is returned as the [D, N] view of the row-major [N, D] tensor (same values/shape as
     # int8:165, zero-copy).
-    return O, lse, q_i8, k_i8.t(), v_i8, sq, sk, sv, k_mean
+    return O, lse, q_i8, k_i8.t(), v_i8, sq, sk, sv, k_mean, q_bf, k_bf
+
+
+def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=None):
+    """Corrected int8 backward; q_bf / k_bf: bf16 images from the forward (computed here if None)."""
+    O = O.to(torch.float16).contiguous()
+    dO = dO.to(torch.float16).contiguous()
+    _lib.require_gpu(dO, O, q_i8)
+    B, H, S, D = O.shape
+    N = B * H * S
+    dev = O.device
+    st = _lib.stream_of(O)
+    k_i8 = k_i8T.t().contiguous()  # [N, D] (a no-op for the view our forward returns)
+    q_i8 = q_i8.contiguous()
+    v_i8 = v_i8.contiguous()
+    dO_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
+    sdO = torch.empty((N // BQ,), dtype=torch.float16, device=dev)
+    LD = torch.empty((N, 2), dtype=torch.float32, device=dev)  # {lse, D} per row
+    dO_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
+    lse = lse.to(torch.float16).contiguous()
+    _lib.call("qattn_int8_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(lse), _lib.ptr(dO_i8),
+              _lib.ptr(sdO), _lib.ptr(LD), _lib.ptr(dO_bf), B * H, S, D, st)
+    # exact bf16 images of the int8 operands read column-wise by the accumulating products
+    if q_bf is None:
+        q_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
+        _lib.call("qattn_i8_to_bf16", _lib.ptr(q_i8), _lib.ptr(q_bf), N * D, st)
+    if k_bf is None:
+        k_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
+        _lib.call("qattn_i8_to_bf16", _lib.ptr(k_i8), _lib.ptr(k_bf), N * D, st)
+    dq = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
+    dk = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
+    dv = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
+    qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
+    sms = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
+    _lib.call("qattn_int8_attn_bwd", _lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8),
+              _lib.ptr(sq.contiguous()), _lib.ptr(k_i8), _lib.ptr(sk.contiguous()),
+              _lib.ptr(v_i8), _lib.ptr(sv.contiguous()), _lib.ptr(LD), _lib.ptr(q_bf),
+              _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
+              B * H, S, D, qks, sms, st)
+    return dq, dk, dv
 
 
 def helion_atten_int8_hl_dot_fwd(
@@ -93,7 +143,7 @@ def helion_atten_int8_hl_dot_fwd(
 ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
            torch.Tensor, torch.Tensor, torch.Tensor, int, int]:
     """int8 forward (int8:101-262): returns (O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv)."""
-    O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, _ = _int8_forward(
+    O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, _, _, _ = _int8_forward(
         q_fp16_input, k_fp16_input, v_fp16_input, smooth=False)
     return O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, BQ, BKV
 
@@ -119,39 +169,8 @@ def helion_atten_int8_hl_dot_bwd(
     """
     if Bq != BQ or Bkv != BKV:
         raise _lib.QAttnError("qattn int8 backward is built for Bq = Bkv = 32")
-    O = O_input_fp16.to(torch.float16).contiguous()
-    dO = dO_input_fp16.to(torch.float16).contiguous()
-    _lib.require_gpu(dO, O, q_bh_int8)
-    B, H, S, D = O.shape
-    N = B * H * S
-    dev = O.device
-    st = _lib.stream_of(O)
-    k_i8 = k_bh_int8_T.t().contiguous()  # [N, D] (a no-op for the view our forward returns)
-    q_i8 = q_bh_int8.contiguous()
-    v_i8 = v_bh_int8.contiguous()
-    dO_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
-    sdO = torch.empty((N // BQ,), dtype=torch.float16, device=dev)
-    LD = torch.empty((N, 2), dtype=torch.float32, device=dev)  # {lse, D} per row
-    lse = lse_input_fp16.to(torch.float16).contiguous()
-    _lib.call("qattn_int8_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(lse), _lib.ptr(dO_i8),
-              _lib.ptr(sdO), _lib.ptr(LD), B * H, S, D, st)
-    # exact bf16 copies of the int8 operands read column-wise by the accumulating products
-    q_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
-    k_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
-    dO_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
-    for src, dst in ((q_i8, q_bf), (k_i8, k_bf), (dO_i8, dO_bf)):
-        _lib.call("qattn_i8_to_bf16", _lib.ptr(src), _lib.ptr(dst), N * D, st)
-    dq = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
-    dk = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
-    dv = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
-    qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
-    sms = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
-    _lib.call("qattn_int8_attn_bwd", _lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8),
-              _lib.ptr(sq_bh_fp16.contiguous()), _lib.ptr(k_i8), _lib.ptr(sk_bh_fp16.contiguous()),
-              _lib.ptr(v_i8), _lib.ptr(sv_bh_fp16.contiguous()), _lib.ptr(LD), _lib.ptr(q_bf),
-              _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
-              B * H, S, D, qks, sms, st)
-    return dq, dk, dv
+    return _int8_backward(dO_input_fp16, q_bh_int8, sq_bh_fp16, k_bh_int8_T, sk_bh_fp16, v_bh_int8,
+                          sv_bh_fp16, O_input_fp16, lse_input_fp16)
 
 
 class SageAttention3_Int8_autograd_function(Function):
@@ -159,26 +178,29 @@ class SageAttention3_Int8_autograd_function(Function):
     (O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv)."""
 
     @staticmethod
-    def forward(q_fp16, k_fp16, v_fp16):
-        O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean = _int8_forward(q_fp16, k_fp16, v_fp16,
-                                                                      smooth=True)
-        return O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, BQ, BKV
-
-    @staticmethod
-    def setup_context(ctx, inputs, output):
-        O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv = output
+    def forward(ctx, q_fp16, k_fp16, v_fp16):
+        # The bf16 images of q_i8 / k_i8 the backward reads come out of the same quantiser pass
+        # when a gradient will be taken (kept on ctx, not returned: the 11-tuple is the reference's).
+        images = any(t.requires_grad for t in (q_fp16, k_fp16, v_fp16))
+        O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean, q_bf, k_bf = _int8_forward(
+            q_fp16, k_fp16, v_fp16, smooth=True, images=images)
         ctx.mark_non_differentiable(lse, k_mean, sq, sk, sv)  # int8:52-56
         ctx.save_for_backward(O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv)  # int8:58-64
-        ctx.args = (Bq, Bkv)
+        ctx.images = (q_bf, k_bf)
+        ctx.args = (BQ, BKV)
+        return O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, BQ, BKV
 
     @staticmethod
     def backward(ctx, dO_fp16, _lse, _k_mean, _q_i8, _k_i8T, _v_i8, _sq, _sk, _sv, _Bq, _Bkv):
         O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv = ctx.saved_tensors
         Bq, Bkv = ctx.args
+        if Bq != BQ or Bkv != BKV:
+            raise _lib.QAttnError("qattn int8 backward is built for Bq = Bkv = 32")
         if dO_fp16 is None:
             dO_fp16 = torch.zeros_like(O)
-        dq, dk, dv = helion_atten_int8_hl_dot_bwd(dO_fp16, q_i8, sq, k_i8T, k_mean, sk, v_i8, sv,
-                                                   O, lse, Bq, Bkv)
+        q_bf, k_bf = ctx.images
+        ctx.images = None
+        dq, dk, dv = _int8_backward(dO_fp16, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf, k_bf)
         return dq, dk, dv
 
 

@@ -60,25 +60,67 @@ QA_DEVICE void quant_operand(const float* x, float inv, float c, v8bf* out) {
 }
 
 // ------------------------------------------------------------------------------------ prep
-// LD[row] = {fp32(lse[row]), fp16(sum_d fp32(fp16(dO*O)))} (int8:360, int8:398)
-template <int D>
-__global__ __launch_bounds__(256) void int8_bwd_ld_kernel(const _Float16* __restrict__ dO,
-                                                          const _Float16* __restrict__ O,
-                                                          const _Float16* __restrict__ lse,
-                                                          float2* __restrict__ LD, long rows) {
-  constexpr int LPR = D / 8;
-  const long row = ((long)blockIdx.x * 256 + threadIdx.x) / LPR;
-  const int c = (threadIdx.x % LPR) * 8;
-  float acc = 0.f;
-  if (row < rows) {
-    const v8h a = *reinterpret_cast<const v8h*>(dO + row * D + c);
-    const v8h b = *reinterpret_cast<const v8h*>(O + row * D + c);
+// One wave per 32-row block of dO (and O), one pass over both:
+//   sdO = f16(amax|dO| / 127), dO_i8 = trunc(f16(dO / sdO))      (int8:372-374, same quantiser)
+//   img = bf16(dO_i8)  (exact; the dV product's transposed-read image; optional)
+//   LD[row] = {f32(lse[row]), f32(f16(sum_d f32(f16(dO*O))))}    (int8:360, int8:398)
+template <int D, bool IMG>
+__global__ __launch_bounds__(256) void int8_bwd_prep_kernel(
+    const _Float16* __restrict__ dO, const _Float16* __restrict__ O, const _Float16* __restrict__ lse,
+    int8_t* __restrict__ idx, _Float16* __restrict__ scale, __bf16* __restrict__ img,
+    float2* __restrict__ LD, long nblocks) {
+  constexpr int ELEMS = 32 * D;
+  constexpr int ITERS = ELEMS / 512;   // 8 halfs per lane per iteration
+  constexpr int TPR = D / 8;           // lanes per row
+  const int lane = threadIdx.x & 63;
+  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= nblocks) return;
+  const _Float16* xb = dO + blk * ELEMS;
+  const _Float16* ob = O + blk * ELEMS;
+  v8h v[ITERS];
+  float amax = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += (float)(_Float16)((float)a[j] * (float)b[j]);
+  for (int i = 0; i < ITERS; ++i) {
+    const int e = (i * 64 + lane) * 8;
+    v[i] = *reinterpret_cast<const v8h*>(xb + e);
+    const v8h o = *reinterpret_cast<const v8h*>(ob + e);
+    float dsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      amax = fmaxf(amax, fabsf((float)v[i][j]));
+      dsum += (float)(_Float16)((float)v[i][j] * (float)o[j]);
+    }
+#pragma unroll
+    for (int m = TPR / 2; m >= 1; m >>= 1) dsum += __shfl_xor(dsum, m);
+    if (lane % TPR == 0) {
+      const long row = blk * 32 + e / D;
+      LD[row] = float2{(float)lse[row], (float)(_Float16)dsum};
+    }
   }
+  amax = wave_max_f(amax);
+  const _Float16 s16 = (_Float16)(amax / 127.0f);
+  const float s = (float)s16;
+  if (lane == 0) scale[blk] = s16;
 #pragma unroll
-  for (int o = LPR / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-  if (row < rows && (threadIdx.x % LPR) == 0) LD[row] = float2{(float)lse[row], (float)(_Float16)acc};
+  for (int i = 0; i < ITERS; ++i) {
+    const int e = (i * 64 + lane) * 8;
+    unsigned lo = 0, hi = 0;
+    float qf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int qi = 0;
+      if (s != 0.f) qi = (int)__builtin_truncf((float)(_Float16)((float)v[i][j] / s));
+      const unsigned b = (unsigned)(qi & 0xff);
+      if (j < 4) lo |= b << (8 * j); else hi |= b << (8 * (j - 4));
+      qf[j] = (float)qi;
+    }
+    *reinterpret_cast<v2u*>(idx + blk * ELEMS + e) = v2u{lo, hi};
+    if constexpr (IMG) {
+      const v4u w = {pk_bf16(qf[0], qf[1]), pk_bf16(qf[2], qf[3]), pk_bf16(qf[4], qf[5]),
+                     pk_bf16(qf[6], qf[7])};
+      *reinterpret_cast<v4u*>(img + blk * ELEMS + e) = w;
+    }
+  }
 }
 // y = bf16(x) for int8 x (exact): 16 bytes in, 32 bytes out per thread
 __global__ __launch_bounds__(256) void i8_to_bf16_kernel(const int8_t* __restrict__ x,
@@ -440,26 +482,25 @@ void int8_bwd_kernel(
 
 using namespace qattn;
 
-extern "C" int qattn_int8_quant(const void* x, void* idx, void* scale, void* deq, const void* kmean,
-                                long rows, int rows_per_head, int head_dim, void* stream);
-
-// dO_i8 / s_dO (per 32-row block, int8:372-374) and LD = {lse, D} per row.
+// dO_i8 / s_dO (per 32-row block, int8:372-374), optional bf16 image of dO_i8, LD = {lse, D} per row.
 extern "C" int qattn_int8_bwd_prep(const void* dO, const void* O, const void* lse, void* dO_i8,
-                                   void* sdO, void* LD, long bh, long seq, int head_dim, void* stream) {
+                                   void* sdO, void* LD, void* dO_bf, long bh, long seq, int head_dim,
+                                   void* stream) {
   if (seq % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  const long rows = bh * seq;
-  if (rows == 0) return 0;
-  int rc = qattn_int8_quant(dO, dO_i8, sdO, nullptr, nullptr, rows, (int)seq, head_dim, stream);
-  if (rc) return rc;
-  const int rpb = 256 / (head_dim / 8);
-  dim3 grid((unsigned)((rows + rpb - 1) / rpb)), block(256);
+  const long nblocks = bh * seq / 32;
+  if (nblocks == 0) return 0;
+  dim3 grid((unsigned)((nblocks + 3) / 4)), block(256);
   hipStream_t st = (hipStream_t)stream;
-  if (head_dim == 128)
-    hipLaunchKernelGGL((int8_bwd_ld_kernel<128>), grid, block, 0, st, (const _Float16*)dO,
-                       (const _Float16*)O, (const _Float16*)lse, (float2*)LD, rows);
-  else
-    hipLaunchKernelGGL((int8_bwd_ld_kernel<64>), grid, block, 0, st, (const _Float16*)dO,
-                       (const _Float16*)O, (const _Float16*)lse, (float2*)LD, rows);
+#define QA_LAUNCH(Dv, IM)                                                                       \
+  hipLaunchKernelGGL((int8_bwd_prep_kernel<Dv, IM>), grid, block, 0, st, (const _Float16*)dO,   \
+                     (const _Float16*)O, (const _Float16*)lse, (int8_t*)dO_i8, (_Float16*)sdO,   \
+                     (__bf16*)dO_bf, (float2*)LD, nblocks)
+  if (head_dim == 128) {
+    if (dO_bf) QA_LAUNCH(128, true); else QA_LAUNCH(128, false);
+  } else {
+    if (dO_bf) QA_LAUNCH(64, true); else QA_LAUNCH(64, false);
+  }
+#undef QA_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -14,10 +14,13 @@
 namespace qattn {
 
 // rows: total rows (multiple of 32); rows_per_head: S (for the k-mean lookup)
-template <int D, bool DEQ, bool SMOOTH>
+// DEQ: also write f16(idx * s) (the forward's P.V operand for v); IMG: also write bf16(idx) (the
+// exact transposed-read image the backward's accumulating products use for q and k).
+template <int D, bool DEQ, bool SMOOTH, bool IMG>
 __global__ __launch_bounds__(256) void quant_block32_kernel(
     const _Float16* __restrict__ x, int8_t* __restrict__ idx, _Float16* __restrict__ scale,
-    _Float16* __restrict__ deq, const _Float16* __restrict__ kmean, long nblocks, int rows_per_head) {
+    _Float16* __restrict__ deq, __bf16* __restrict__ img, const _Float16* __restrict__ kmean,
+    long nblocks, int rows_per_head) {
   constexpr int ELEMS = 32 * D;        // elements per block
   constexpr int ITERS = ELEMS / 512;   // 8 halfs per lane per iteration
   const int lane = threadIdx.x & 63;
@@ -50,6 +53,7 @@ __global__ __launch_bounds__(256) void quant_block32_kernel(
     const int e = (i * 64 + lane) * 8;
     unsigned lo = 0, hi = 0;
     v8h dq;
+    float qf[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       int qi = 0;
@@ -57,25 +61,43 @@ __global__ __launch_bounds__(256) void quant_block32_kernel(
       const unsigned b = (unsigned)(qi & 0xff);
       if (j < 4) lo |= b << (8 * j); else hi |= b << (8 * (j - 4));
       if constexpr (DEQ) dq[j] = (_Float16)((float)qi * s);
+      qf[j] = (float)qi;
     }
     *reinterpret_cast<v2u*>(idx + blk * ELEMS + e) = v2u{lo, hi};
     if constexpr (DEQ) *reinterpret_cast<v8h*>(deq + blk * ELEMS + e) = dq;
+    if constexpr (IMG) {
+      const v4u w = {pk_bf16(qf[0], qf[1]), pk_bf16(qf[2], qf[3]), pk_bf16(qf[4], qf[5]),
+                     pk_bf16(qf[6], qf[7])};
+      *reinterpret_cast<v4u*>(img + blk * ELEMS + e) = w;
+    }
   }
 }
 
 // k_mean[bh][d] = fp16( sum_s fp32(k[bh][s][d]) / S )   (eager `k.mean(-2)` in fp16, fp32 accumulate)
+// One 1024-thread workgroup per head; 4 independent 16-B loads in flight per thread.
 template <int D>
-__global__ __launch_bounds__(256) void kmean_kernel(const _Float16* __restrict__ k,
-                                                    _Float16* __restrict__ kmean, int S) {
+__global__ __launch_bounds__(1024) void kmean_kernel(const _Float16* __restrict__ k,
+                                                     _Float16* __restrict__ kmean, int S) {
   constexpr int TPR = D / 8;           // threads per row (8 halfs each)
-  constexpr int RPI = 256 / TPR;       // rows per iteration
+  constexpr int RPI = 1024 / TPR;      // rows per step
+  constexpr int U = 4;                 // steps unrolled
   __shared__ float part[RPI][D + 1];
   const int bh = blockIdx.x;
   const int t = threadIdx.x;
   const int c = (t % TPR) * 8, r0 = t / TPR;
   const _Float16* kb = k + (long)bh * S * D;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = r0; r < S; r += RPI) {
+  int r = r0;
+  for (; r + (U - 1) * RPI < S; r += U * RPI) {
+    v8h x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = *reinterpret_cast<const v8h*>(kb + (long)(r + u * RPI) * D + c);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)x[u][j];
+  }
+  for (; r < S; r += RPI) {
     const v8h x = *reinterpret_cast<const v8h*>(kb + (long)r * D + c);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] += (float)x[j];
@@ -84,9 +106,9 @@ __global__ __launch_bounds__(256) void kmean_kernel(const _Float16* __restrict__
   for (int j = 0; j < 8; ++j) part[r0][c + j] = acc[j];
   __syncthreads();
   if (t < D) {
-    float s = 0.f;
-    for (int r = 0; r < RPI; ++r) s += part[r][t];
-    kmean[(long)bh * D + t] = (_Float16)(s / (float)S);
+    float sum = 0.f;
+    for (int i = 0; i < RPI; ++i) sum += part[i][t];
+    kmean[(long)bh * D + t] = (_Float16)(sum / (float)S);
   }
 }
 
@@ -94,8 +116,9 @@ __global__ __launch_bounds__(256) void kmean_kernel(const _Float16* __restrict__
 
 using namespace qattn;
 
-extern "C" int qattn_int8_quant(const void* x, void* idx, void* scale, void* deq, const void* kmean,
-                                long rows, int rows_per_head, int head_dim, void* stream) {
+extern "C" int qattn_int8_quant_img(const void* x, void* idx, void* scale, void* deq, void* img,
+                                    const void* kmean, long rows, int rows_per_head, int head_dim,
+                                    void* stream) {
   if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
   if (kmean && rows_per_head % 32 != 0) return 1;
   const long nblocks = rows / 32;
@@ -106,18 +129,30 @@ extern "C" int qattn_int8_quant(const void* x, void* idx, void* scale, void* deq
   auto I = (int8_t*)idx;
   auto Sc = (_Float16*)scale;
   auto Q = (_Float16*)deq;
+  auto B = (__bf16*)img;
   auto M = (const _Float16*)kmean;
-#define QA_LAUNCH(Dv, DQ, SM) \
-  hipLaunchKernelGGL((quant_block32_kernel<Dv, DQ, SM>), grid, block, 0, st, X, I, Sc, Q, M, nblocks, rows_per_head)
-  if (head_dim == 128) {
-    if (deq) { if (kmean) QA_LAUNCH(128, true, true); else QA_LAUNCH(128, true, false); }
-    else { if (kmean) QA_LAUNCH(128, false, true); else QA_LAUNCH(128, false, false); }
-  } else {
-    if (deq) { if (kmean) QA_LAUNCH(64, true, true); else QA_LAUNCH(64, true, false); }
-    else { if (kmean) QA_LAUNCH(64, false, true); else QA_LAUNCH(64, false, false); }
+#define QA_LAUNCH(Dv, DQ, SM, IM)                                                                    \
+  hipLaunchKernelGGL((quant_block32_kernel<Dv, DQ, SM, IM>), grid, block, 0, st, X, I, Sc, Q, B, M, \
+                     nblocks, rows_per_head)
+#define QA_LAUNCH_D(Dv)                                                                             \
+  if (deq) {                                                                                        \
+    if (kmean) QA_LAUNCH(Dv, true, true, false); else QA_LAUNCH(Dv, true, false, false);            \
+  } else if (img) {                                                                                 \
+    if (kmean) QA_LAUNCH(Dv, false, true, true); else QA_LAUNCH(Dv, false, false, true);            \
+  } else {                                                                                          \
+    if (kmean) QA_LAUNCH(Dv, false, true, false); else QA_LAUNCH(Dv, false, false, false);          \
   }
+  if (deq && img) return 1;   // one extra output per launch
+  if (head_dim == 128) { QA_LAUNCH_D(128) } else { QA_LAUNCH_D(64) }
+#undef QA_LAUNCH_D
 #undef QA_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_int8_quant(const void* x, void* idx, void* scale, void* deq, const void* kmean,
+                                long rows, int rows_per_head, int head_dim, void* stream) {
+  return qattn_int8_quant_img(x, idx, scale, deq, nullptr, kmean, rows, rows_per_head, head_dim,
+                              stream);
 }
 
 extern "C" int qattn_kmean(const void* k, void* kmean, long bh, long seq, int head_dim, void* stream) {
@@ -125,10 +160,10 @@ extern "C" int qattn_kmean(const void* k, void* kmean, long bh, long seq, int he
   if (bh == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (head_dim == 128)
-    hipLaunchKernelGGL((kmean_kernel<128>), dim3((unsigned)bh), dim3(256), 0, st, (const _Float16*)k,
+    hipLaunchKernelGGL((kmean_kernel<128>), dim3((unsigned)bh), dim3(1024), 0, st, (const _Float16*)k,
                        (_Float16*)kmean, (int)seq);
   else
-    hipLaunchKernelGGL((kmean_kernel<64>), dim3((unsigned)bh), dim3(256), 0, st, (const _Float16*)k,
+    hipLaunchKernelGGL((kmean_kernel<64>), dim3((unsigned)bh), dim3(1024), 0, st, (const _Float16*)k,
                        (_Float16*)kmean, (int)seq);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

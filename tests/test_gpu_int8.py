@@ -130,3 +130,35 @@ def test_sage_attention_autograd(lib):
     torch.nn.functional.mse_loss(R.baseline_pytorch_attention(qf, kf, vf, 64, False), gt).backward()
     for a, b in ((qd.grad, qf.grad), (kd.grad, kf.grad), (vd.grad, vf.grad)):
         assert _rel(a.cpu(), b) <= 0.15
+
+
+def test_quant_image_and_bwd_prep(lib):
+    """qattn_int8_quant_img writes bf16(idx) exactly; qattn_int8_bwd_prep (one pass) gives the same
+    dO indices/scales as the quantiser, bf16(dO_i8), and LD = {lse, f16(rowsum f16(dO*O))}."""
+    from quantizedattention_amd import _lib
+    g = torch.Generator().manual_seed(77)
+    B, H, S, D = 1, 2, 128, 128
+    N = B * H * S
+    x = torch.randn((N, D), generator=g).half().cuda()
+    O = torch.randn((N, D), generator=g).half().cuda()
+    lse = (torch.rand(N, generator=g) * 8).half().cuda()
+    P, st = _lib.ptr, _lib.stream_of(x)
+    idx = torch.empty((N, D), dtype=torch.int8, device="cuda")
+    sc = torch.empty((N // 32,), dtype=torch.float16, device="cuda")
+    img = torch.empty((N, D), dtype=torch.bfloat16, device="cuda")
+    _lib.call("qattn_int8_quant_img", P(x), P(idx), P(sc), None, P(img), None, N, S, D, st)
+    ridx, rsc = R.quant_blocks(x.cpu())
+    torch.cuda.synchronize()
+    assert torch.equal(idx.cpu(), ridx) and torch.equal(sc.cpu().view(torch.int16), rsc.view(torch.int16))
+    assert torch.equal(img.cpu(), ridx.to(torch.bfloat16))
+    di = torch.empty_like(idx)
+    ds = torch.empty_like(sc)
+    dimg = torch.empty_like(img)
+    LD = torch.empty((N, 2), dtype=torch.float32, device="cuda")
+    _lib.call("qattn_int8_bwd_prep", P(x), P(O), P(lse), P(di), P(ds), P(LD), P(dimg), B * H, S, D, st)
+    torch.cuda.synchronize()
+    assert torch.equal(di.cpu(), ridx) and torch.equal(ds.cpu().view(torch.int16), rsc.view(torch.int16))
+    assert torch.equal(dimg.cpu(), ridx.to(torch.bfloat16))
+    Dref = (x.cpu().float() * O.cpu().float()).half().float().sum(-1).half().float()
+    assert torch.equal(LD[:, 0].cpu(), lse.cpu().float())
+    assert (LD[:, 1].cpu() - Dref).abs().max().item() <= 2 * 2.0 ** -10 * Dref.abs().max().item()

@@ -12,7 +12,7 @@ from quantizedattention_amd.attention_int8 import _int8_forward  # noqa: E402
 B, H, S, D = (int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4,32,4096,128").split(","))
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn((B, H, S, D), device="cuda", generator=g).half() for _ in range(3))
-O, lse, qi, kiT, vi, sq, sk, sv, _ = _int8_forward(q, k, v, False)
+O, lse, qi, kiT, vi, sq, sk, sv, _, _, _ = _int8_forward(q, k, v, False)
 N = B * H * S
 vdq = torch.empty((N, D), dtype=torch.float16, device="cuda")
 st = _lib.stream_of(q)

@@ -7,7 +7,7 @@ B, H, S, D = 4, 32, 4096, 128
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn((B, H, S, D), device="cuda", generator=g).half() for _ in range(3))
 N = B * H * S; P = _lib.ptr; st = _lib.stream_of(q)
-O, lse, qi, kiT, vi, sq, sk, sv, km = _int8_forward(q, k, v, False)
+O, lse, qi, kiT, vi, sq, sk, sv, km, _, _ = _int8_forward(q, k, v, False)
 ki = kiT.t(); vdq = torch.empty((N, D), dtype=torch.float16, device="cuda")
 _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))

@@ -30,14 +30,14 @@ P = _lib.ptr
 st = _lib.stream_of(q)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
 sms = float(torch.tensor(1 / math.sqrt(D), dtype=torch.float32))
-O, lse, qi, kiT, vi, sq, sk, sv, km = _int8_forward(q, k, v, False)
+O, lse, qi, kiT, vi, sq, sk, sv, km, _, _ = _int8_forward(q, k, v, False)
 ki = kiT.t()
 vdq = torch.empty((N, D), dtype=torch.float16, device="cuda")
 _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 dOi = torch.empty((N, D), dtype=torch.int8, device="cuda")
 sdO = torch.empty((N // 32,), dtype=torch.float16, device="cuda")
 LD = torch.empty((N, 2), dtype=torch.float32, device="cuda")
-_lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(lse), P(dOi), P(sdO), P(LD), B * H, S, D, st)
+_lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(lse), P(dOi), P(sdO), P(LD), None, B * H, S, D, st)
 qb, kb, ob = (torch.empty((N, D), dtype=torch.bfloat16, device="cuda") for _ in range(3))
 for a_, b_ in ((qi, qb), (ki, kb), (dOi, ob)):
     _lib.call("qattn_i8_to_bf16", P(a_), P(b_), N * D, st)

@@ -21,7 +21,7 @@ ops = 4*B*H*S*S*D
 t = timeit(lambda: helion_atten_int8_hl_dot_fwd(q,k,v))
 print(f"int8 fwd full  (4,32,4096,128): {t*1e3:.1f} us  {ops/t/1e9:.1f} TOPS  ({ops/t/1e9/5033*100:.1f}% of 5.03 POPS)")
 # attention kernel alone
-O, lse, qi, kiT, vi, sq, sk, sv, _ = _int8_forward(q,k,v,False)
+O, lse, qi, kiT, vi, sq, sk, sv, _, _, _ = _int8_forward(q,k,v,False)
 N = B*H*S
 vdq = torch.empty((N,D), dtype=torch.float16, device='cuda')
 st = _lib.stream_of(q)
