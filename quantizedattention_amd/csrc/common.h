@@ -303,6 +303,51 @@ QA_DEVICE v8s ds_read_tr16_x2(const void* addr0, const void* addr1) {
   return __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// ---------------------------------------------------------------- row-major tile stores
+// A wave's 32-row x D output tile in the transposed 32x32 MFMA layout (acc[b][r] holds element
+// d = 32b + 8(r>>2) + 4h + (r&3) of row l&31) written as whole rows: staged through the wave's own
+// LDS region (row pitch padded by 16 B: the 8-/16-B per-row writes are bank-conflict-free), then
+// read back 16 B per lane and stored with fully coalesced 16-B global stores (a 1-KiB span per
+// instruction).  Storing straight from the MFMA layout touches 32 rows per instruction with 8-16 B
+// each, which made the epilogue dominate short kernels.
+template <int D, typename T>
+struct RowTile {
+  static constexpr int PITCH = D * (int)sizeof(T) + 16;
+  static constexpr int BYTES = 32 * PITCH;
+};
+template <int D, typename T>
+QA_DEVICE void store_rows(const v16f* acc, float sc, char* lds, T* dst_row0, int lane) {
+  using RT = RowTile<D, T>;
+  const int h = lane >> 5, c32 = lane & 31;
+#pragma unroll
+  for (int b = 0; b < D / 32; ++b) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      char* p = lds + c32 * RT::PITCH + (32 * b + 8 * g + 4 * h) * (int)sizeof(T);
+      if constexpr (sizeof(T) == 2) {
+        v4h w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * sc);
+        *reinterpret_cast<v4h*>(p) = w;
+      } else {
+        v4f w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = acc[b][4 * g + j] * sc;
+        *reinterpret_cast<v4f*>(p) = w;
+      }
+    }
+  }
+  constexpr int CPR = D * (int)sizeof(T) / 16;   // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;                  // rows per instruction
+  const int r = lane / CPR, c = lane % CPR;
+#pragma unroll
+  for (int i = 0; i < 32 / RPI; ++i) {
+    const int row = i * RPI + r;
+    const v4u v = *reinterpret_cast<const v4u*>(lds + row * RT::PITCH + 16 * c);
+    *reinterpret_cast<v4u*>(reinterpret_cast<char*>(dst_row0) + (long)row * D * (long)sizeof(T) + 16 * c) = v;
+  }
+}
+
 // Workgroup -> (head, q-tile) remap that keeps every q-tile of one head on one XCD
 // (blocks b and b+8 share an XCD under round-robin dispatch; speed only, never correctness).
 QA_DEVICE void xcd_remap(int bid, int nq, int nbh, int& bh, int& qt) {

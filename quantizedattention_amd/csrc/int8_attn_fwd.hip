@@ -117,6 +117,11 @@ struct DmaPlan {
 // (compiles to v_max3_i32).  Deliberately NOT inline asm: its inputs are MFMA results, and hipcc's
 // hazard recogniser inserts the MFMA-result -> VALU wait states only for instructions it emits itself.
 QA_DEVICE int imax3(int a, int b, int c) { return max(max(a, b), c); }
+#if defined(QA_FWD_STAMP)
+__device__ unsigned long long g_fwd_stamps[32 * 4 * 64 * 8];
+__device__ unsigned long long g_fwd_wginfo[8192 * 4];
+#endif
+
 // Per-wave softmax state between the two halves of a tile.
 struct SmTile {
   v2h d[8];       // f16(S - rm) for the 16 scores of this lane
@@ -198,12 +203,14 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
 
   auto slot_of = [&](int t) -> const char* { return smem + (STREAM ? (t & 3) : 0) * C::SLOT; };
 
-  // S^T tile t into an int32 accumulator
-  auto qk = [&](int t) -> v16i {
+  // S^T tile t into an int32 accumulator: fragment loads and MFMAs separately, so the K loads of
+  // tile t+1 can be issued ahead of the V-operand loads of tile t
+  auto qk_load = [&](int t, v4i* kf) {
     const char* kl = slot_of(t);
-    v4i kf[C::NKS];
 #pragma unroll
     for (int s = 0; s < C::NKS; ++s) kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s]);
+  };
+  auto qk_mma = [&](const v4i* kf) -> v16i {
     v16i acc;
     if constexpr (AB == 3) {
 #pragma unroll
@@ -214,6 +221,11 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       for (int s = 1; s < C::NKS; ++s) acc = mfma_i8(kf[s], qf[s], acc);
     }
     return acc;
+  };
+  auto qk = [&](int t) -> v16i {
+    v4i kf[C::NKS];
+    qk_load(t, kf);
+    return qk_mma(kf);
   };
 
   // first half of the softmax of a tile (c = sq*sk*qks of the tile):
@@ -233,12 +245,13 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       auto r = __builtin_amdgcn_permlane32_swap((unsigned)mx, (unsigned)mx, false, false);
       mx = max((int)r[0], (int)r[1]);
     }
-    const _Float16 rm = mul_mix((float)mx, c);
-    float af[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) af[i] = (float)acc[i];
+    // S = f16(f32(acc * c)) (int8:200-203: fp32 products, then fp16); v_mul + v_cvt_pk_f16_f32 is
+    // cheaper than v_fma_mix (tools/ubench) and rounds like the reference's fp32 chain
+    const _Float16 rm = (_Float16)((float)mx * c);
     v2h s2[8];
-    fma_mix8(af, c, 0.0f, s2);           // S = f16(acc * c)          (int8:200-203)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      s2[j] = __builtin_bit_cast(v2h, pk_f16((float)acc[2 * j] * c, (float)acc[2 * j + 1] * c));
     const v2h rm2 = {rm, rm};
 #pragma unroll
     for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;   // f16(S - rm)  (int8:211, 232-236)
@@ -263,9 +276,15 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
     v2h e[8], w[8];
     exp2_pk4(&st.d[0], &e[0]);
     exp2_pk4(&st.d[4], &e[4]);
+    // row-sum of e: one packed f16 add level (pairs of values <= 1), then fp32; v_dot2c_f32_f16 is
+    // avoided: beside MFMAs it issues ~5x slower than plain VALU (tools/ubench)
     float esum = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) esum = __builtin_amdgcn_fdot2(e[j], one2, esum, false);
+    for (int j = 0; j < 4; ++j) {
+      const v2h p = e[2 * j] + e[2 * j + 1];
+      esum += (float)p[0] + (float)p[1];
+    }
+    (void)one2;
     l += esum * st.er;
     const v2h sp2 = {st.sp, st.sp};
     const _Float16 nsp = (_Float16)(-1024.0f) * st.sp;
@@ -343,21 +362,40 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
   // Steady state: one basic block per tile (except the rare running-max rescale).  The last
   // iteration computes QK / SM1 of a duplicate of the last tile (its slot holds a clamped re-load):
   // harmless (its row max cannot move m) and it keeps the loop body branch-free.
+#if defined(QA_FWD_STAMP)
+  unsigned long long wg_t0 = __builtin_amdgcn_s_memtime();
+  // timing build: per-phase s_memtime stamps of workgroups 0..31, tiles 0..63
+  unsigned long long* stamp = g_fwd_stamps + ((long)(blockIdx.x * C::WAVES + wave) * 64) * 8;
+  const bool do_stamp = blockIdx.x < 32;
+#define QA_STAMP(k)                                                                  \
+  if (do_stamp && t < 64 && lane == 0) {                                             \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    stamp[t * 8 + (k)] = __builtin_amdgcn_s_memtime();                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+  }
+#else
+#define QA_STAMP(k)
+#endif
   for (int t = 0; t < nt; ++t) {
+    QA_STAMP(0)
     if constexpr (STREAM) {
 #if defined(QA_FWD_NOBAR)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::IPW) : "memory");   // timing experiment only
 #else
       ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
 #endif
+      QA_STAMP(1)
       dma.issue(smem_lds + ((t + 3) & 3) * C::SLOT, min(t + 3, nt - 1));
     }
     if (active) {
       const int tn = min(t + 1, nt - 1);
       const float cn = cq * (float)sk_lds[tn];
+      v4i kf[C::NKS];
+      qk_load(tn, kf);
       v8h va[2 * C::NDB];
       pv_load(t, va);
-      const v16i nacc = qk(tn);
+      const v16i nacc = qk_mma(kf);
+      QA_STAMP(2)
       v4u pw[2];
       if constexpr (SOFTMAX) {
         sm2(st, pw);
@@ -367,34 +405,40 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) pw[s][j] = __builtin_bit_cast(unsigned, st.d[4 * s + j]) & 0x3fff3fffu;
       }
+      QA_STAMP(3)
       pv_mma(va, pw);
+      QA_STAMP(4)
       if constexpr (SOFTMAX) {
         const _Float16 rm = sm1a(nacc, cn, st);
+        QA_STAMP(5)
         sm1b(rm, st);
       } else {
         st.d[0] = __builtin_bit_cast(v2h, nacc[0]);
       }
+      QA_STAMP(6)
     }
   }
+#undef QA_STAMP
   if constexpr (STREAM) vmcnt_wait_all();
+  __syncthreads();   // every wave is done with the ring: its slots become the output staging area
 
   if (!active) return;
+#if defined(QA_FWD_STAMP)
+  if (tid == 0 && blockIdx.x < 8192) {   // per workgroup: start, end, HW_ID, XCC_ID
+    unsigned long long* w = g_fwd_wginfo + 4L * blockIdx.x;
+    w[0] = wg_t0;
+    w[1] = __builtin_amdgcn_s_memtime();
+    w[2] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID, 32 bits
+    w[3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // HW_REG_XCC_ID
+  }
+#endif
   // ---------------- epilogue: lse = fp16(m + fp16(log2 l)); O = fp16(O / l)   (int8:252-257)
   l = pair_sum(l);
   const long qrow = head_row0 + q0 + c32;
   if (h == 0) lse[qrow] = (_Float16)((float)m + (float)(_Float16)log2_f32(l));
-  const float il = 1.0f / l;
-  _Float16* orow = out + qrow * D;
-#pragma unroll
-  for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      v4h w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = (_Float16)(o[b][4 * g + j] * il);
-      *reinterpret_cast<v4h*>(orow + 32 * b + 8 * g + 4 * h) = w;
-    }
-  }
+  static_assert(C::WAVES * RowTile<D, _Float16>::BYTES <= C::NSLOT * C::SLOT, "staging fits the ring");
+  store_rows<D, _Float16>(o, 1.0f / l, smem + wave * RowTile<D, _Float16>::BYTES,
+                          out + (head_row0 + q0) * D, lane);
 }
 
 template <int D, int AB>
@@ -441,3 +485,11 @@ extern "C" int qattn_int8_attn_fwd_ablate(const void* q_i8, const void* sq, cons
     default: return launch_fwd<128, 0>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
   }
 }
+
+#if defined(QA_FWD_STAMP)
+extern "C" int qattn_fwd_stamps(void* stamps, void* wginfo) {
+  hipMemcpyFromSymbol(stamps, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps));
+  hipMemcpyFromSymbol(wginfo, HIP_SYMBOL(g_fwd_wginfo), sizeof(g_fwd_wginfo));
+  return 0;
+}
+#endif

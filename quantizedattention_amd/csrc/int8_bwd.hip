@@ -162,6 +162,9 @@ __global__ __launch_bounds__(256) void i8_to_bf16_kernel(const int8_t* __restric
 // quantisation of tile t, the fp32 P/dS of tile t+1 are computed beside the bf16 MFMAs of tile t);
 // ROLE_DKV (two fp32 accumulators) runs unpipelined with 8 waves per workgroup instead.
 enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
+#ifndef QA_DKV_PIPE
+#define QA_DKV_PIPE 0
+#endif
 
 template <int D, int ROLE>
 struct BwdCfg {
@@ -435,6 +438,38 @@ void int8_bwd_kernel(
         quantise(X, ROLE == ROLE_DV ? so_p(t) : so_ds(t), op);
         accumulate(acc, ta, op);
         values(tn, sa, pa, X, X);
+      }
+    }
+  } else if constexpr (QA_DKV_PIPE) {
+    // DKV pipelined: carry the quantised bf16 operands of tile t (16 VGPRs) into iteration t, whose
+    // int8 products for tile t+1 are issued first and whose fp32 values of t+1 are computed beside
+    // the bf16 MFMAs of tile t
+    v8bf opS[2], opP[2];
+    if (active) {
+      v16i sa, pa;
+      products(0, sa, pa);
+      float P[16], dS[16];
+      values(0, sa, pa, P, dS);
+      quantise(dS, so_ds(0), opS);
+      quantise(P, so_p(0), opP);
+    }
+    for (int t = 0; t < nt; ++t) {
+      ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
+      dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
+                min(t + G::NSLOT - 1, nt - 1), lane);
+      if (active) {
+        const int tn = min(t + 1, nt - 1);
+        v16i sa, pa;
+        products(tn, sa, pa);
+        v8bf ta[2 * C::NDB];
+        tr_load(t, G::TR, ta);
+        accumulate(acc, ta, opS);          // dK += q^T dS
+        tr_load(t, G::TR2, ta);
+        accumulate(acc2, ta, opP);         // dV += dO^T P
+        float P[16], dS[16];
+        values(tn, sa, pa, P, dS);
+        quantise(dS, so_ds(tn), opS);
+        quantise(P, so_p(tn), opP);
       }
     }
   } else {
