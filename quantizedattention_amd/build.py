@@ -24,9 +24,18 @@ CFLAGS = [
     "-fno-gpu-rdc", "-Wno-unused-result", f"-I{INCLUDE}",
 ]
 
+# Per-source extras.  The bf16 forward keeps its fp32 softmax scalar (-fno-slp-vectorize: the SLP
+# vectoriser otherwise emits v_pk_mul/add_f32, which issue through the matrix pipe and wait ~38
+# cycles behind a co-resident wave's MFMA, tools/ubench) and runs with IEEE mode off
+# (-mno-amdgpu-ieee, valid with -fno-honor-nans: no NaN reaches it), so v_max needs no canonicalising
+# v_max x,x of its bit-cast inputs.
+FILE_FLAGS = {
+    "bf16_fwd.hip": ["-fno-slp-vectorize", "-mno-amdgpu-ieee", "-fno-honor-nans"],
+}
+
 
 def _compile(src: Path, obj: Path) -> str:
-    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")

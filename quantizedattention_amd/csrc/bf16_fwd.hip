@@ -10,194 +10,334 @@
 //   P  = bf16(exp2(bf16(bf16(S*qks) - m')));  r = bf16(exp2(bf16(m - m')))       bf16:267-276
 //   l  = l*r + sum P;  O = O*r + P.V  (bf16 MFMA, fp32 accumulate)              bf16:279-285
 //   lse = m + log2 l;  O /= l                                                   bf16:288-294
+// Every bf16 rounding is the hardware RNE v_cvt_pk_bf16_f32 on pairs (unpacked with one shift /
+// mask each); "#{S >= thr} > 1" is evaluated as "second-largest S of the row >= thr", with the
+// row's top two values carried by v_max / v_med3 (the largest is the row max the rule needs anyway).
 //
-// Structure (same as int8_attn_fwd.hip): 4 waves x 32 query rows per workgroup, keys streamed in
-// 64-key blocks through a 2-stage LDS ring, swapped QK^T (keys in registers, one query per lane
-// pair), P fed straight from the accumulator registers into the PV MFMA (B operand), V read
-// column-wise with ds_read_b64_tr_b16.  One 16-key sub-tile == one k-step of the 32x32x16 PV MFMA.
+// Structure (as int8_attn_fwd.hip): 4 waves x 32 query rows per workgroup; 32-key K/V tiles
+// stream through a 4-slot LDS ring filled by buffer LDS-DMA (one barrier per tile); swapped QK^T
+// (keys in registers, one query per lane pair) so P feeds the PV MFMA straight from registers;
+// V read column-wise with ds_read_b64_tr_b16.  One 16-key sub-tile == one k-step of the
+// 32x32x16 PV MFMA.  Software pipeline: the QK^T MFMAs of tile t+1 are issued before the
+// softmax of tile t.
+#include <type_traits>
+
 #include "common.h"
+
+#ifndef QA_BF_AB
+#define QA_BF_AB 0
+#endif
+#ifndef QA_BF_MUNPACK
+#define QA_BF_MUNPACK 0
+#endif
 
 namespace qattn {
 
 template <int D>
 struct Bf16FwdCfg {
-  static constexpr int KB = 64;
-  static constexpr int ROWB = 2 * D;            // bytes per K/V row
+  static constexpr int WAVES = 4;
+  static constexpr int QROWS = 32 * WAVES;
+  static constexpr int KT = 32;                 // keys per ring slot
+  static constexpr int NSLOT = 4;
+  static constexpr int ROWB = 2 * D;            // bytes per K / V row
   static constexpr int NCH = ROWB / 16;         // 16-B chunks per row
-  static constexpr int TILE = KB * ROWB;        // bytes per K (or V) block
-  static constexpr int STAGE = 2 * TILE;
-  static constexpr int NKS = D / 16;            // f16 k-steps for QK^T
+  static constexpr int TILE = KT * ROWB;        // bytes per K (or V) tile
+  static constexpr int SLOT = 2 * TILE;
+  static constexpr int NKS = D / 16;            // f16 k-steps of QK^T
   static constexpr int NDB = D / 32;
-  static constexpr int LOADS = TILE / (256 * 16);
-  static constexpr int K_SHIFT = (D == 128) ? 0 : 1;   // swizzle = (row >> K_SHIFT) & (NCH-1)
-  static constexpr int V_SHIFT = (D == 128) ? 2 : 1;   // swizzle = (row & 3) << V_SHIFT
+  static constexpr int PIECES = SLOT / 1024;    // 1-KiB LDS-DMA pieces per slot
+  static constexpr int IPW = PIECES / WAVES;
+  static constexpr int K_SHIFT = (D == 128) ? 0 : 1;   // K swizzle = (row >> K_SHIFT) & (NCH-1)
+  static constexpr int V_SHIFT = (D == 128) ? 2 : 1;   // V swizzle = (row & 3) << V_SHIFT
+  static constexpr int STAGE_BYTES = WAVES * RowTile<D, float>::BYTES;
+  static constexpr int LDS = (NSLOT * SLOT > STAGE_BYTES) ? NSLOT * SLOT : STAGE_BYTES;
 };
 
 template <int D>
-QA_DEVICE int kf_off(int row, int ch) {
+QA_DEVICE int bk_sw(int row) {
   using C = Bf16FwdCfg<D>;
-  return row * C::ROWB + 16 * (ch ^ ((row >> C::K_SHIFT) & (C::NCH - 1)));
+  return (row >> C::K_SHIFT) & (C::NCH - 1);
 }
 template <int D>
-QA_DEVICE int vf_off(int row, int ch) {
+QA_DEVICE int bv_sw(int row) {
   using C = Bf16FwdCfg<D>;
-  return row * C::ROWB + 16 * (ch ^ ((row & 3) << C::V_SHIFT));
+  return (row & 3) << C::V_SHIFT;
 }
 
-// A operand (V^T, 32 d x 16 keys) of one PV k-step via two transposed reads.
-template <int D, typename T8>
-QA_DEVICE T8 load_vt_frag(const char* vl, int key_base, int b, int lane) {
-  const int h = lane >> 5, gg = (lane >> 4) & 1, i16 = lane & 15;
-  const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
-  const int key = key_base + 4 * h + (i16 >> 2);
-  const int ch = d / 8, within = (d % 8) * 2;
-  const v8s a = ds_read_tr16_x2(vl + vf_off<D>(key, ch) + within,
-                                vl + vf_off<D>(key + 8, ch) + within);
-  return __builtin_bit_cast(T8, a);
-}
-
+// LDS-DMA plan of one 32-key tile: piece p < TILE/1024 is K, the rest V; lane-constant offsets.
 template <int D>
+struct Bf16Dma {
+  using C = Bf16FwdCfg<D>;
+  unsigned voff[C::IPW];
+  unsigned lds_off[C::IPW];
+  v4u rsrc[C::IPW];
+  QA_DEVICE void init(int wave, int lane, int Sk, const void* kbase, const void* vbase) {
+    constexpr int RPI = 64 / C::NCH;
+    constexpr int KP = C::TILE / 1024;
+#pragma unroll
+    for (int i = 0; i < C::IPW; ++i) {
+      const int p = wave + C::WAVES * i;
+      const bool isv = p >= KP;
+      const int piece = isv ? p - KP : p;
+      const int row = piece * RPI + lane / C::NCH, c = lane % C::NCH;
+      voff[i] = row * C::ROWB + 16 * (c ^ (isv ? bv_sw<D>(row) : bk_sw<D>(row)));
+      lds_off[i] = (isv ? C::TILE : 0) + piece * 1024;
+      rsrc[i] = make_rsrc(isv ? vbase : kbase, (unsigned)Sk * C::ROWB);
+    }
+  }
+  QA_DEVICE void issue(unsigned slot_lds, int tile) const {
+#pragma unroll
+    for (int i = 0; i < C::IPW; ++i)
+      dma16_buf(rsrc[i], voff[i], (unsigned)tile * C::TILE, slot_lds + lds_off[i]);
+  }
+};
+
+// bf16 RNE of two fp32 values, returned unpacked as fp32 (and the packed pair)
+QA_DEVICE unsigned rne2(float a, float b, float& ra, float& rb) {
+  const unsigned w = pk_bf16(a, b);
+  ra = __uint_as_float(w << 16);
+  rb = __uint_as_float(w & 0xffff0000u);
+  return w;
+}
+QA_DEVICE float rne1(float a) { return __uint_as_float(pk_bf16(a, a) & 0xffff0000u); }
+
+template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void bf16_fwd_kernel(
     const _Float16* __restrict__ q, const _Float16* __restrict__ k, const __bf16* __restrict__ v,
-    float* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, int causal, float qks) {
+    float* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, float qks) {
   using C = Bf16FwdCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nq = (Sq + 127) / 128;
+  const int nq = (Sq + C::QROWS - 1) / C::QROWS;
   int bh, qt;
   xcd_remap(blockIdx.x, nq, BH, bh, qt);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const int q0 = qt * 128 + wave * 32;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int q0 = qt * C::QROWS + wave * 32;
   const bool active = q0 < Sq;
   const int qidx = q0 + c32;                     // this lane's query row
-  const float thr_eps = 0.00099945068359375f;  // bf16(1e-3): eager `bf16 - 1e-3` rounds the scalar (bf16:248)
+  const float thr_eps = 0.00099945068359375f;    // bf16(1e-3): eager `bf16 - 1e-3` rounds the scalar (bf16:248)
+  const int nt = Sk / C::KT;
+
+  Bf16Dma<D> dma;
+  dma.init(wave, lane, Sk, k + (long)bh * Sk * D, v + (long)bh * Sk * D);
+  const unsigned smem_lds = lds_addr(smem);
+#pragma unroll
+  for (int i = 0; i < C::NSLOT - 1; ++i) dma.issue(smem_lds + i * C::SLOT, min(i, nt - 1));
 
   v8h qf[C::NKS];
-  if (active) {
-    const _Float16* qrow = q + ((long)bh * Sq + qidx) * D + 8 * h;
+  {
+    // waves past the end (ragged Sq) run on a clamped copy of the last row and store nothing, so
+    // the tile loop has no per-wave branch
+    const _Float16* qrow = q + ((long)bh * Sq + min(qidx, Sq - 1)) * D + 8 * h;
 #pragma unroll
     for (int s = 0; s < C::NKS; ++s) qf[s] = *reinterpret_cast<const v8h*>(qrow + 16 * s);
+  }
+  // lane-constant LDS offsets: K A-operand chunk (2s+h) of key row c32; V^T A-operand per d block
+  int koff[C::NKS], voff[C::NDB];
+#pragma unroll
+  for (int s = 0; s < C::NKS; ++s) koff[s] = c32 * C::ROWB + 16 * ((2 * s + h) ^ bk_sw<D>(c32));
+  {
+    const int gg = (lane >> 4) & 1, i16 = lane & 15;
+    const int key_a = 4 * h + (i16 >> 2);
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) {
+      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
+      voff[b] = C::TILE + key_a * C::ROWB + 16 * ((d / 8) ^ bv_sw<D>(key_a)) + (d % 8) * 2;
+    }
   }
   v16f o[C::NDB];
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) o[b] = v16f{};
   float m = -INFINITY;   // bf16-valued
-  float l = 1.0f;
-
-  const char* kbase = reinterpret_cast<const char*>(k + (long)bh * Sk * D);
-  const char* vbase = reinterpret_cast<const char*>(v + (long)bh * Sk * D);
-  const int nkb = (Sk + C::KB - 1) / C::KB;
-
-  v4i kst[C::LOADS], vst[C::LOADS];
-  auto stage_load = [&](int kb) {
-    const int key0 = kb * C::KB;
+  // l (bf16:198, initial 1 wiped by r = 0 on the first sub-tile) is accumulated by the matrix core:
+  // lacc = lacc*r + ones.P, every register of lane l holding l of query l&31 (the VALU is the
+  // bottleneck, the MFMA pipe has room)
+  v16f lacc;
 #pragma unroll
-    for (int i = 0; i < C::LOADS; ++i) {
-      const int e = i * 256 + tid, row = e / C::NCH, ch = e % C::NCH;
-      const bool ok = key0 + row < Sk;
-      const long off = (long)(key0 + row) * C::ROWB + 16 * ch;
-      kst[i] = ok ? *reinterpret_cast<const v4i*>(kbase + off) : v4i{0, 0, 0, 0};
-      vst[i] = ok ? *reinterpret_cast<const v4i*>(vbase + off) : v4i{0, 0, 0, 0};
-    }
+  for (int i = 0; i < 16; ++i) lacc[i] = 1.0f;
+  v8bf ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
+#if QA_BF_MUNPACK
+  // Widening on the matrix core: C = Sel.B with Sel[i][k] = (i == (k&3) + 8((k&7)>>2) + 4(k>>3))
+  // returns, in registers 0..7 of every lane, the lane's own eight 16-bit B elements as exact fp32
+  // (1*x + 0s), in element order.  Replaces the VALU unpack (shift / mask, or v_cvt_f32_f16) of
+  // every packed pair; the VALU is this kernel's bottleneck, the MFMA pipe has room.
+  v8h sel_h;
+  v8bf sel_b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bool one = c32 == (e & 3) + 8 * (e >> 2) + 4 * h;
+    sel_h[e] = one ? (_Float16)1.0f : (_Float16)0.0f;
+    sel_b[e] = one ? (__bf16)1.0f : (__bf16)0.0f;
+  }
+#endif
+
+  // ring slots are compile-time constants (the tile loop is unrolled by NSLOT) so every LDS
+  // address is a lane-constant VGPR plus an instruction offset
+  auto qk = [&](auto SLc) -> v16f {
+    const char* kl = smem + decltype(SLc)::value * C::SLOT;
+    v16f acc = v16f{};
+#pragma unroll
+    for (int s = 0; s < C::NKS; ++s)
+      acc = mfma_f16(*reinterpret_cast<const v8h*>(kl + koff[s]), qf[s], acc);
+    return acc;
   };
-  auto stage_store = [&](int buf) {
-    char* kl = smem + buf * C::STAGE;
-    char* vl = kl + C::TILE;
-#pragma unroll
-    for (int i = 0; i < C::LOADS; ++i) {
-      const int e = i * 256 + tid, row = e / C::NCH, ch = e % C::NCH;
-      *reinterpret_cast<v4i*>(kl + kf_off<D>(row, ch)) = kst[i];
-      *reinterpret_cast<v4i*>(vl + vf_off<D>(row, ch)) = vst[i];
-    }
+  // One 16-key sub-tile u of tile t (acc registers 8u .. 8u+7) in three phases, ordered per tile
+  // as A0 A1 B0 B1 C0 C1 so the two sub-tiles' independent work shares one branch-free block:
+  //   A: S = bf16(fp16(acc)), causal fill, the row's top two (independent of m)
+  //   B: beta rule, P (bf16 pairs) and r (serial in m)
+  //   C: rescale of O and l when some r != 1 (uniform branch), l += ones.P, O += P.V
+  struct Sub {
+    float s[8];
+    float M1, M2;
+    v4u pk;
+    float r;
   };
-
-  stage_load(0);
-  stage_store(0);
-  __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
-    if (kb + 1 < nkb) stage_load(kb + 1);
-    const char* kl = smem + (kb & 1) * C::STAGE;
-    const char* vl = kl + C::TILE;
-    const int ntile = min(2, (Sk - kb * C::KB) / 32);
-    if (active) {
-      for (int u = 0; u < ntile; ++u) {
-        const int key_t0 = kb * C::KB + 32 * u;
-        v16f acc = v16f{};
+  const float inf = INFINITY;
+  auto phase_a = [&](Sub& x, int t, int u, const v16f& acc) {
+#if QA_BF_MUNPACK
+    v4u w;
 #pragma unroll
-        for (int s = 0; s < C::NKS; ++s) {
-          const v8h kf = *reinterpret_cast<const v8h*>(kl + kf_off<D>(32 * u + c32, 2 * s + h));
-          acc = mfma_f16(kf, qf[s], acc);
-        }
-        // S = bf16(fp16(acc)); causal fill -126 where q - k <= 0
-        const bool need_mask = causal && (key_t0 + 31 >= q0);  // some (q, key) of the tile has q - key <= 0
+    for (int j = 0; j < 8; j += 2) w[j / 2] = pk_f16(acc[8 * u + j], acc[8 * u + j + 1]);
+    const v16f f = mfma_f16(sel_h, __builtin_bit_cast(v8h, w), v16f{});
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float s = rne_bf16((float)(_Float16)acc[i]);
-          if (need_mask) {
-            const int key = key_t0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (qidx - key <= 0) s = -126.0f;
-          }
-          acc[i] = s;
-        }
+    for (int j = 0; j < 8; j += 2) w[j / 2] = pk_bf16(f[j], f[j + 1]);
+    const v16f sb = mfma_bf16(sel_b, __builtin_bit_cast(v8bf, w), v16f{});
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          float rl = -INFINITY;
+    for (int j = 0; j < 8; ++j) x.s[j] = sb[j];
+#else
 #pragma unroll
-          for (int j = 0; j < 8; ++j) rl = fmaxf(rl, acc[8 * t + j]);
-          const float rmax = fmaxf(rl, xor32_f(rl));
-          float nm = fmaxf(m, rne_bf16(rmax * qks));
-          const float thr = rne_bf16(nm - thr_eps);
-          int cl = 0;
+    for (int j = 0; j < 8; j += 2) {
+      const unsigned hh = pk_f16(acc[8 * u + j], acc[8 * u + j + 1]);
+      const v2h p = __builtin_bit_cast(v2h, hh);
+      rne2((float)p[0], (float)p[1], x.s[j], x.s[j + 1]);
+    }
+#endif
+    const int key_t0 = t * C::KT + 16 * u;
+    if (CAUSAL && key_t0 + 15 >= q0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) cl += (acc[8 * t + j] >= thr) ? 1 : 0;
-          const int cnt = cl + __shfl_xor(cl, 32);
-          if (cnt > 1) {
-            if (nm > 0.f) nm = rne_bf16(2.0f * nm);
-            else if (nm < 0.f) nm = 0.f;
-          }
-          float lt = 0.f;
-          float p[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            p[j] = rne_bf16(exp2_f32(rne_bf16(rne_bf16(acc[8 * t + j] * qks) - nm)));
-            lt += p[j];
-          }
-          lt += xor32_f(lt);
-          const float r = rne_bf16(exp2_f32(rne_bf16(m - nm)));
-          m = nm;
-          l = l * r + lt;
-          if (__ballot(r != 1.0f)) {
-#pragma unroll
-            for (int b = 0; b < C::NDB; ++b) o[b] *= r;
-          }
-          v4u pk;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pk[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
-          const v8bf pb = __builtin_bit_cast(v8bf, pk);
-#pragma unroll
-          for (int b = 0; b < C::NDB; ++b) {
-            const v8bf a = load_vt_frag<D, v8bf>(vl, 32 * u + 16 * t, b, lane);
-            o[b] = mfma_bf16(a, pb, o[b]);
-          }
-        }
+      for (int j = 0; j < 8; ++j) {
+        const int key = key_t0 + (j & 3) + 8 * (j >> 2) + 4 * h;
+        x.s[j] = (qidx - key <= 0) ? -126.0f : x.s[j];
       }
     }
-    if (kb + 1 < nkb) stage_store((kb + 1) & 1);
-    __syncthreads();
-  }
-  if (!active) return;
-  const long row = (long)bh * Sq + qidx;
-  if (h == 0) lse[row] = m + log2_f32(l);
-  float* orow = out + row * D;
+    // top two (8 here, 8 in lane l^32); fmed3(a, b, +-inf) = max / min in one instruction
+    float m1 = __builtin_amdgcn_fmed3f(x.s[0], x.s[1], inf), m2 = __builtin_amdgcn_fmed3f(x.s[0], x.s[1], -inf);
 #pragma unroll
-  for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      v4f w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = o[b][4 * g + j] / l;
-      *reinterpret_cast<v4f*>(orow + 32 * b + 8 * g + 4 * h) = w;
+    for (int j = 2; j < 8; ++j) {
+      m2 = __builtin_amdgcn_fmed3f(m1, m2, x.s[j]);
+      m1 = __builtin_amdgcn_fmed3f(m1, x.s[j], inf);
     }
+    const auto x1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
+    const auto x2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m2), __float_as_uint(m2), false, false);
+    const float a1 = __uint_as_float(x1[0]), b1 = __uint_as_float(x1[1]);
+    x.M1 = __builtin_amdgcn_fmed3f(a1, b1, inf);
+    x.M2 = __builtin_amdgcn_fmed3f(   // max(min(m1, o1), m2, o2)
+        __builtin_amdgcn_fmed3f(__builtin_amdgcn_fmed3f(a1, b1, -inf), __uint_as_float(x2[0]), inf),
+        __uint_as_float(x2[1]), inf);
+  };
+  auto phase_b = [&](Sub& x) {
+    float nm = __builtin_amdgcn_fmed3f(m, rne1(x.M1 * qks), inf);   // bf16:236-239
+    const float thr = rne1(nm - thr_eps);                            // bf16:248
+    // #{S >= thr} > 1  <=>  second largest >= thr:  m' = 2m' (m' > 0) | 0 (m' < 0)   bf16:248-264
+    const float dbl = (nm > 0.f) ? rne1(2.0f * nm) : 0.0f;
+    nm = (x.M2 >= thr && nm != 0.f) ? dbl : nm;
+    // P = bf16(exp2(bf16(bf16(S*qks) - nm))).  Scalar fp32 on purpose: v_pk_*_f32 issue through
+    // the matrix pipe and stall ~38 cycles behind the co-resident wave's MFMAs (tools/ubench).
+#if QA_BF_MUNPACK
+    v4u w;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) w[j / 2] = pk_bf16(x.s[j] * qks, x.s[j + 1] * qks);
+    const v16f a = mfma_bf16(sel_b, __builtin_bit_cast(v8bf, w), v16f{});
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) w[j / 2] = pk_bf16(a[j] - nm, a[j + 1] - nm);
+    const v16f e = mfma_bf16(sel_b, __builtin_bit_cast(v8bf, w), v16f{});
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) x.pk[j / 2] = pk_bf16(exp2_f32(e[j]), exp2_f32(e[j + 1]));
+#else
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      float a, b;
+      rne2(x.s[j] * qks, x.s[j + 1] * qks, a, b);
+      rne2(a - nm, b - nm, a, b);
+      x.pk[j / 2] = pk_bf16(exp2_f32(a), exp2_f32(b));
+    }
+#endif
+    x.r = rne1(exp2_f32(rne1(m - nm)));                              // bf16:276
+    m = nm;
+  };
+  auto phase_c = [&](auto SLc, const Sub& x, int u) {
+    if (__ballot(x.r != 1.0f)) {
+#pragma unroll
+      for (int b = 0; b < C::NDB; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[b][i] = o[b][i] * x.r;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) lacc[i] = lacc[i] * x.r;
+    }
+    const v8bf pb8 = __builtin_bit_cast(v8bf, x.pk);
+#if QA_BF_AB == 2   // timing: no P.V / l products
+    lacc[u] += __builtin_bit_cast(float, x.pk[0]);
+    return;
+#endif
+    lacc = mfma_bf16(ones, pb8, lacc);                               // l = l*r + sum P   (bf16:279)
+    const char* vl = smem + decltype(SLc)::value * C::SLOT;
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) {
+      const char* a = vl + voff[b] + 16 * u * C::ROWB;
+      const v8bf va = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * C::ROWB));
+      o[b] = mfma_bf16(va, pb8, o[b]);                               // bf16:285
+    }
+  };
+
+  vmem_drain();
+  __syncthreads();
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  v16f acc = v16f{};
+  acc = qk(I0{});
+  // tile t lives in slot t & 3; at tile t the slot (t+1)&3 holds tile min(t+1, nt-1)
+  auto step = [&](auto SLc, auto NXc, auto FRc, int t) {
+    ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
+    dma.issue(smem_lds + decltype(FRc)::value * C::SLOT, min(t + 3, nt - 1));
+    {
+      const v16f nacc = qk(NXc);
+      Sub x0, x1;
+#if QA_BF_AB == 1   // timing skeleton: no softmax
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x0.pk[j] = pk_bf16(acc[2 * j], acc[2 * j + 1]);
+        x1.pk[j] = pk_bf16(acc[8 + 2 * j], acc[9 + 2 * j]);
+      }
+      x0.r = x1.r = 1.0f;
+#else
+      phase_a(x0, t, 0, acc);
+      phase_a(x1, t, 1, acc);
+      phase_b(x0);
+      phase_b(x1);
+#endif
+      phase_c(SLc, x0, 0);
+      phase_c(SLc, x1, 1);
+      acc = nacc;
+    }
+  };
+  for (int t = 0; t < nt; t += 4) {
+    step(I0{}, I1{}, I3{}, t);
+    if (t + 1 < nt) step(I1{}, I2{}, I0{}, t + 1);
+    if (t + 2 < nt) step(I2{}, I3{}, I1{}, t + 2);
+    if (t + 3 < nt) step(I3{}, I0{}, I2{}, t + 3);
   }
+  vmcnt_wait_all();
+  __syncthreads();   // the ring becomes the output staging area
+  if (!active) return;
+  const long row0 = (long)bh * Sq + q0;
+  const float l = lacc[0];
+  if (h == 0) lse[row0 + c32] = m + log2_f32(l);                 // bf16:288
+  store_rows<D, float>(o, 1.0f / l, smem + wave * RowTile<D, float>::BYTES, out + row0 * D, lane);
 }
 
 }  // namespace qattn
@@ -208,14 +348,22 @@ extern "C" int qattn_bf16_fwd(const void* q, const void* k, const void* v, void*
                               long sq, long sk, int head_dim, int causal, float qks, void* stream) {
   if (sq % 32 != 0 || sk % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
   if (bh == 0 || sq == 0) return 0;
-  const int nq = (int)((sq + 127) / 128);
-  dim3 grid((unsigned)(nq * bh)), block(256);
   hipStream_t st = (hipStream_t)stream;
-#define QA_LAUNCH(Dv)                                                                          \
-  hipLaunchKernelGGL((bf16_fwd_kernel<Dv>), grid, block, 2 * Bf16FwdCfg<Dv>::STAGE, st,        \
-                     (const _Float16*)q, (const _Float16*)k, (const __bf16*)v, (float*)out,      \
-                     (float*)lse, (int)bh, (int)sq, (int)sk, causal, qks)
-  if (head_dim == 128) QA_LAUNCH(128); else QA_LAUNCH(64);
+#define QA_LAUNCH(Dv, CV)                                                                        \
+  {                                                                                              \
+    using C = Bf16FwdCfg<Dv>;                                                                    \
+    const int nq = (int)((sq + C::QROWS - 1) / C::QROWS);                                        \
+    hipFuncSetAttribute((const void*)bf16_fwd_kernel<Dv, CV>,                                    \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);                     \
+    hipLaunchKernelGGL((bf16_fwd_kernel<Dv, CV>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), \
+                       C::LDS, st, (const _Float16*)q, (const _Float16*)k, (const __bf16*)v,     \
+                       (float*)out, (float*)lse, (int)bh, (int)sq, (int)sk, qks);                \
+  }
+  if (head_dim == 128) {
+    if (causal) QA_LAUNCH(128, true) else QA_LAUNCH(128, false)
+  } else {
+    if (causal) QA_LAUNCH(64, true) else QA_LAUNCH(64, false)
+  }
 #undef QA_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

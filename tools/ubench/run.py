@@ -10,7 +10,8 @@ lib = ctypes.CDLL(os.path.join(here, "libubench.so"))
 lib.ubench.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int]
 names = ["v_mul_f32", "v_fma_f32", "v_cvt_f32_i32", "v_trunc_f32", "v_exp_f32", "v_cvt_pk_bf16_f32",
          "v_max3_f32", "v_exp_f16", "v_pk_fma_f16", "v_pk_add_f16", "v_dot2c_f32_f16",
-         "v_fma_mixlo_f16", "v_max_f32", "v_mov_b32", "v_add_u32", "v_cvt_f32_f16"]
+         "v_fma_mixlo_f16", "v_max_f32", "v_mov_b32", "v_add_u32", "v_cvt_f32_f16", "v_pk_mul_f32", "v_pk_add_f32", "v_pk_fma_f32",
+         "v_cvt_f32_bf16", "v_med3_f32", "v_dot2_f32_bf16"]
 iters = 2000
 nb = 256
 for k, name in enumerate(names):

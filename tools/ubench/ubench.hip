@@ -52,6 +52,33 @@ DEF(13, U16("v_mov_b32"))
 DEF(14, L16("v_add_u32"))
 DEF(15, U16("v_cvt_f32_f16"))
 
+// packed-fp32 kinds: 8 independent 64-bit register pairs, each instruction used twice per block
+#define DEF64(K, OP)                                                                       \
+  template <>                                                                              \
+  __device__ __forceinline__ void block<K>(float (&r)[16], int (&ri)[16]) {               \
+    double d[8];                                                                           \
+    for (int i = 0; i < 8; ++i) d[i] = __builtin_bit_cast(double, (float __attribute__((ext_vector_type(2)))){r[2 * i], r[2 * i + 1]}); \
+    asm volatile(OP OP                                                                     \
+                 : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]),  \
+                   "+v"(d[6]), "+v"(d[7]));                                                \
+    for (int i = 0; i < 8; ++i) {                                                          \
+      auto v = __builtin_bit_cast(float __attribute__((ext_vector_type(2))), d[i]);        \
+      r[2 * i] = v[0]; r[2 * i + 1] = v[1];                                                \
+    }                                                                                      \
+  }
+#define L8(I)                                                                               \
+  I " %0, %0, %0\n" I " %1, %1, %1\n" I " %2, %2, %2\n" I " %3, %3, %3\n" I " %4, %4, %4\n"     \
+  I " %5, %5, %5\n" I " %6, %6, %6\n" I " %7, %7, %7\n"
+#define T8(I)                                                                               \
+  I " %0, %0, %0, %0\n" I " %1, %1, %1, %1\n" I " %2, %2, %2, %2\n" I " %3, %3, %3, %3\n"         \
+  I " %4, %4, %4, %4\n" I " %5, %5, %5, %5\n" I " %6, %6, %6, %6\n" I " %7, %7, %7, %7\n"
+DEF64(16, L8("v_pk_mul_f32"))
+DEF64(17, L8("v_pk_add_f32"))
+DEF64(18, T8("v_pk_fma_f32"))
+DEF(19, U16("v_cvt_f32_bf16"))
+DEF(20, T16("v_med3_f32"))
+DEF(21, T16("v_dot2_f32_bf16"))
+
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
@@ -89,7 +116,7 @@ extern "C" int ubench(int kind, int waves_per_simd, int mfma_waves, int iters, l
                       int nblocks) {
   dim3 grid(nblocks), block(64 * 4 * waves_per_simd);
 #define K(N) case N: hipLaunchKernelGGL((ubench_kernel<N>), grid, block, 0, 0, out, iters, mfma_waves); break;
-  switch (kind) { K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15) }
+  switch (kind) { K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15) K(16) K(17) K(18) K(19) K(20) K(21) }
 #undef K
   return hipDeviceSynchronize() == hipSuccess ? 0 : 2;
 }
