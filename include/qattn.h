@@ -130,6 +130,20 @@ int qattn_jvp_fwd(const void* q, const void* k, const void* v, const void* tq, c
                   const void* tv, void* out, void* tout, void* lse, long bh, long sq, long sk,
                   int head_dim, int flags, float qks, float sm, void* stream);
 
+/* fp32-accurate JVP (the reference's fp32 contract, SURVEY §8c "fp32 mode"): every operand is given
+ * as two bf16 images x = hi + lo (qattn_split_bf16) and every product runs as
+ * hi*hi + hi*lo + lo*hi + lo*lo on the bf16 MFMA (exact up to the 2^-17 split residual, fp32
+ * accumulation).  Same outputs and
+ * conventions as qattn_jvp_fwd; sq % 32 == 0, sk % 32 == 0. */
+int qattn_jvp_fwd_x3(const void* q_hi, const void* q_lo, const void* k_hi, const void* k_lo,
+                     const void* v_hi, const void* v_lo, const void* tq_hi, const void* tq_lo,
+                     const void* tk_hi, const void* tk_lo, const void* tv_hi, const void* tv_lo,
+                     void* out, void* tout, void* lse, long bh, long sq, long sk, int head_dim,
+                     float qks, float sm, void* stream);
+
+/* hi = bf16(x), lo = bf16(x - hi) (both round-to-nearest-even) for n fp32 elements, n % 4 == 0. */
+int qattn_split_bf16(const void* x, void* hi, void* lo, long n, void* stream);
+
 /* ---------------------------------------------------------------- diagnostics (not product API) */
 
 /* qattn_int8_attn_fwd with parts of the tile pipeline disabled (ab = 0 full, 1 no softmax,

@@ -3,10 +3,16 @@
 Public names:
   helion_attention_jvp_forward_fp32   attention_jvp.py:24-195  (q,k,v,tq,tk,tv) -> (O, tO, lse)
   baseline_pytorch_attention          attention_jvp.py:197-215 (non-causal)
+  AttentionJVP_autograd_function      SURVEY §8f N1: torch.autograd.Function whose ``jvp`` staticmethod
+  attention_jvp                       routes forward-mode AD (torch.func.jvp, torch.autograd.forward_ad)
+                                      to the kernel (README.md:19-22 of the reference promises this use)
 
-The kernel multiplies bf16 operands on MFMA with fp32 accumulation and fp32 softmax state
-(BASELINE.json config 5: "attention_jvp fwd ... in bf16").  fp32 inputs are accepted and rounded to
-bf16 on entry; outputs are fp32 as in the reference.
+Two numeric modes, chosen by the input dtype (outputs are fp32 in both, as in the reference):
+  * bf16 inputs (BASELINE.json config 5): bf16 MFMA operands, fp32 accumulation and softmax state.
+  * fp32 inputs: the fp32-accurate mode.  Every operand is split into two bf16 images (hi + lo,
+    qattn_split_bf16) and each product runs as hi*hi + hi*lo + lo*hi on the MFMA (qattn_jvp_fwd_x3),
+    which keeps ~16 significand bits per product (fp32 mode <= 1e-5 vs torch.func.jvp).
+Other dtypes are cast to fp32 first.
 """
 from __future__ import annotations
 
@@ -17,7 +23,8 @@ import torch
 from . import _lib
 from ._baseline import baseline_pytorch_attention as _baseline
 
-__all__ = ["helion_attention_jvp_forward_fp32", "baseline_pytorch_attention"]
+__all__ = ["helion_attention_jvp_forward_fp32", "baseline_pytorch_attention",
+           "AttentionJVP_autograd_function", "attention_jvp"]
 
 
 def baseline_pytorch_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
@@ -37,21 +44,90 @@ def helion_attention_jvp_forward_fp32(q_fp32_input, k_fp32_input, v_fp32_input,
     ins = (q_fp32_input, k_fp32_input, v_fp32_input, tan_q_fp32_input, tan_k_fp32_input,
            tan_v_fp32_input)
     _lib.require_gpu(*ins)
-    if q_tokens % 32 or k_tokens % 64:
-        raise _lib.QAttnError("qattn jvp: q tokens must be a multiple of 32, k tokens of 64")
+    if q_tokens % 32 or k_tokens % 32:
+        raise _lib.QAttnError("qattn jvp: q and k tokens must be multiples of 32")
     if q_head_dim not in (64, 128):
         raise _lib.QAttnError("qattn jvp: head_dim must be 64 or 128")
     for t, ref in zip(ins[3:], ins[:3]):
         if t.shape != ref.shape:
             raise _lib.QAttnError("qattn jvp: tangents must have the primals' shapes")
-    q, k, v, tq, tk, tv = (t.to(torch.bfloat16).contiguous() for t in ins)
-    B, H, S, D = q.shape
-    O = torch.empty((B, H, S, D), dtype=torch.float32, device=q.device)
+    B, H, S, D = q_fp32_input.shape
+    dev = q_fp32_input.device
+    O = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
     tO = torch.empty_like(O)
-    lse = torch.empty((B * H, S), dtype=torch.float32, device=q.device)
+    lse = torch.empty((B * H, S), dtype=torch.float32, device=dev)
     qks = float(torch.tensor(1.0 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
     sm = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
-    _lib.call("qattn_jvp_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(tq), _lib.ptr(tk),
-              _lib.ptr(tv), _lib.ptr(O), _lib.ptr(tO), _lib.ptr(lse), B * H, S, k_tokens, D, 0, qks,
-              sm, _lib.stream_of(q))
+    st = _lib.stream_of(q_fp32_input)
+    if all(t.dtype == torch.bfloat16 for t in ins):
+        if k_tokens % 64:
+            raise _lib.QAttnError("qattn jvp: k tokens must be a multiple of 64 for bf16 inputs")
+        q, k, v, tq, tk, tv = (t.contiguous() for t in ins)
+        _lib.call("qattn_jvp_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(tq), _lib.ptr(tk),
+                  _lib.ptr(tv), _lib.ptr(O), _lib.ptr(tO), _lib.ptr(lse), B * H, S, k_tokens, D, 0, qks,
+                  sm, st)
+        return O, tO, lse
+    imgs = []
+    for t in ins:
+        x = t.to(torch.float32).contiguous()
+        hi = torch.empty(x.shape, dtype=torch.bfloat16, device=dev)
+        lo = torch.empty_like(hi)
+        _lib.call("qattn_split_bf16", _lib.ptr(x), _lib.ptr(hi), _lib.ptr(lo), x.numel(), st)
+        imgs += [hi, lo]
+    _lib.call("qattn_jvp_fwd_x3", *(_lib.ptr(t) for t in imgs), _lib.ptr(O), _lib.ptr(tO), _lib.ptr(lse),
+              B * H, S, k_tokens, D, qks, sm, st)
     return O, tO, lse
+
+
+def _plain(t: torch.Tensor) -> torch.Tensor:
+    from torch._C._functorch import get_unwrapped, is_functorch_wrapped_tensor
+    while is_functorch_wrapped_tensor(t):
+        t = get_unwrapped(t)
+    return t
+
+
+class AttentionJVP_autograd_function(torch.autograd.Function):
+    """Attention O = softmax(q k^T / sqrt(D)) v whose forward-mode derivative is the kernel's tO.
+
+    ``torch.func.jvp(attention_jvp, (q, k, v), (tq, tk, tv))`` and ``torch.autograd.forward_ad``
+    dual tensors both dispatch to :meth:`jvp`.  The forward runs the same kernel with zero tangents
+    (so O matches the one the jvp call would produce); reverse mode is not provided, as in the
+    reference, which has no backward for this path.
+    """
+
+    @staticmethod
+    def forward(q, k, v):
+        q, k, v = _plain(q), _plain(k), _plain(v)
+        with torch._C._DisableFuncTorch():
+            O, _tO, _lse = helion_attention_jvp_forward_fp32(q, k, v, torch.zeros_like(q),
+                                                             torch.zeros_like(k), torch.zeros_like(v))
+        return O
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        q, k, v = inputs
+        ctx.save_for_forward(q, k, v)
+
+    @staticmethod
+    def jvp(ctx, tq, tk, tv):
+        # under torch.func.jvp the saved primals and the tangents arrive as functorch wrappers
+        # (no storage) and new tensors would be wrapped too: the kernel runs on the plain tensors
+        # with functorch disabled, and torch re-wraps the plain tO
+        q, k, v = (_plain(t) for t in ctx.saved_tensors)
+        tq, tk, tv = (None if t is None else _plain(t) for t in (tq, tk, tv))
+        with torch._C._DisableFuncTorch():
+            tq = torch.zeros_like(q) if tq is None else tq.to(q.dtype)
+            tk = torch.zeros_like(k) if tk is None else tk.to(k.dtype)
+            tv = torch.zeros_like(v) if tv is None else tv.to(v.dtype)
+        with torch._C._DisableFuncTorch():   # plain allocations for the kernel's buffers
+            _O, tO, _lse = helion_attention_jvp_forward_fp32(q, k, v, tq, tk, tv)
+        return tO
+
+    @staticmethod
+    def backward(ctx, grad_O):
+        raise RuntimeError("qattn jvp: reverse mode is not provided (forward-mode AD only)")
+
+
+def attention_jvp(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """O fp32 [B,H,S,D]; differentiable in forward mode through the HIP tangent kernel."""
+    return AttentionJVP_autograd_function.apply(q, k, v)

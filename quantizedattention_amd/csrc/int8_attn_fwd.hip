@@ -131,7 +131,8 @@ struct SmTile {
 
 // AB (diagnostic timing builds only, never dispatched by the API): 1 = no softmax VALU,
 // 2 = no PV MFMA, 3 = no QK^T MFMA, 4 = no K/V streaming (ring slot 0 reused, no barriers),
-// 5 = 4 + no softmax.  Outputs of AB != 0 are meaningless.
+// 5 = 4 + no softmax, 6 = 1 + half the V-operand LDS reads, 7 = 1 + half the K-operand LDS reads.
+// Outputs of AB != 0 are meaningless.
 template <int D, int AB = 0>
 __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
     _Float16* __restrict__ lse, int BH, int S, float qks) {
   using C = Int8FwdCfg<D>;
   constexpr bool STREAM = AB != 4 && AB != 5;
-  constexpr bool SOFTMAX = AB != 1 && AB != 5;
+  constexpr bool SOFTMAX = AB != 1 && AB != 5 && AB != 6 && AB != 7;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   _Float16* sk_lds = reinterpret_cast<_Float16*>(smem + C::NSLOT * C::SLOT);
 
@@ -208,7 +209,10 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
   auto qk_load = [&](int t, v4i* kf) {
     const char* kl = slot_of(t);
 #pragma unroll
-    for (int s = 0; s < C::NKS; ++s) kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s]);
+    for (int s = 0; s < C::NKS; ++s) {
+      if (AB == 7 && s >= C::NKS / 2) kf[s] = kf[s - C::NKS / 2] + 1;   // half the K reads (timing)
+      else kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s]);
+    }
   };
   auto qk_mma = [&](const v4i* kf) -> v16i {
     v16i acc;
@@ -319,6 +323,7 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b) {
         const char* a = vl + voff[b] + 16 * s * 2 * D;
+        if (AB == 6 && s == 1) { va[s * C::NDB + b] = va[b] * (_Float16)2.0f; continue; }   // half the V reads (timing)
         va[s * C::NDB + b] = __builtin_bit_cast(v8h, ds_read_tr16_x2(a, a + 8 * 2 * D));
       }
   };
@@ -394,8 +399,17 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       qk_load(tn, kf);
       v8h va[2 * C::NDB];
       pv_load(t, va);
+#if defined(QA_FWD_SB)
+      __builtin_amdgcn_sched_barrier(0);   // LDS reads issue first; the softmax VALU covers their latency
+      v4u pw[2];
+      sm2(st, pw);
+      __builtin_amdgcn_sched_barrier(0);
       const v16i nacc = qk_mma(kf);
+#else
+      const v16i nacc = qk_mma(kf);
+#endif
       QA_STAMP(2)
+#if !defined(QA_FWD_SB)
       v4u pw[2];
       if constexpr (SOFTMAX) {
         sm2(st, pw);
@@ -405,6 +419,7 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) pw[s][j] = __builtin_bit_cast(unsigned, st.d[4 * s + j]) & 0x3fff3fffu;
       }
+#endif
       QA_STAMP(3)
       pv_mma(va, pw);
       QA_STAMP(4)
@@ -482,6 +497,8 @@ extern "C" int qattn_int8_attn_fwd_ablate(const void* q_i8, const void* sq, cons
     case 3: return launch_fwd<128, 3>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
     case 4: return launch_fwd<128, 4>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
     case 5: return launch_fwd<128, 5>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
+    case 6: return launch_fwd<128, 6>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
+    case 7: return launch_fwd<128, 7>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
     default: return launch_fwd<128, 0>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
   }
 }

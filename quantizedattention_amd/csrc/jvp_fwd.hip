@@ -16,13 +16,19 @@
 
 namespace qattn {
 
-template <int D>
+// X3 = the fp32-accurate mode: every fp32 operand x is carried as two bf16 images x = hi + lo
+// (hi = bf16(x), lo = bf16(x - hi), qattn_split_bf16) and each product as
+// hi*hi + hi*lo + lo*hi + lo*lo, exact up to the split residual |x - hi - lo| <= 2^-17 |x|.
+// 4x the MFMAs of the bf16 mode.  Measured vs torch.func.jvp in float64 (tools/jvp_err.py): O within
+// 6e-6, tO within 8e-6 at max|tO| = 1.35 (dropping lo*lo: tO 2.7e-5).
+template <int D, bool X3>
 struct JvpCfg {
-  static constexpr int KB = 64;
+  static constexpr int KB = X3 ? 32 : 64;     // keys per stage
+  static constexpr int NIMG = X3 ? 2 : 1;     // bf16 images per operand
   static constexpr int ROWB = 2 * D;
   static constexpr int NCH = ROWB / 16;
   static constexpr int TILE = KB * ROWB;
-  static constexpr int STAGE = 4 * TILE;  // K, tK, V, tV
+  static constexpr int STAGE = 4 * NIMG * TILE;  // K, tK, V, tV (x hi/lo)
   static constexpr int NKS = D / 16;
   static constexpr int NDB = D / 32;
 };
@@ -31,12 +37,12 @@ QA_DEVICE int jrow_sw(int row) { return (D == 128) ? (row & 15) : ((row >> 1) & 
 template <int D>
 QA_DEVICE int jtr_sw(int row) { return (row & 3) << ((D == 128) ? 2 : 1); }
 
-// LDS-DMA one [64 rows][ROWB] tile: lane-linear destination, swizzled source chunk.
-template <int D, bool TR>
+// LDS-DMA one [KB rows][ROWB] tile: lane-linear destination, swizzled source chunk.
+template <int D, bool X3, bool TR>
 QA_DEVICE void dma_tile(const char* gsrc, char* lds_tile, int wave, int lane) {
-  using C = JvpCfg<D>;
-  constexpr int RPI = 64 / C::NCH;       // rows per wave-instruction (1 KiB)
-  constexpr int IPW = C::NCH / 4;        // instructions per wave (4 waves)
+  using C = JvpCfg<D, X3>;
+  constexpr int RPI = 64 / C::NCH;                 // rows per wave-instruction (1 KiB)
+  constexpr int IPW = C::TILE / 1024 / 4;          // instructions per wave (4 waves)
 #pragma unroll
   for (int i = 0; i < IPW; ++i) {
     const int inst = wave * IPW + i;
@@ -49,39 +55,55 @@ QA_DEVICE void dma_tile(const char* gsrc, char* lds_tile, int wave, int lane) {
 
 template <int D>
 QA_DEVICE v8bf jtr_frag(const char* base, int row_base, int b, int lane) {
-  using C = JvpCfg<D>;
+  constexpr int ROWB = 2 * D;
   const int h = lane >> 5, gg = (lane >> 4) & 1, i16 = lane & 15;
   const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
   const int row = row_base + 4 * h + (i16 >> 2);
   const int ch = d / 8, within = (d % 8) * 2;
   return __builtin_bit_cast(
-      v8bf, ds_read_tr16_x2(base + row * C::ROWB + 16 * (ch ^ jtr_sw<D>(row)) + within,
-                            base + (row + 8) * C::ROWB + 16 * (ch ^ jtr_sw<D>(row + 8)) + within));
+      v8bf, ds_read_tr16_x2(base + row * ROWB + 16 * (ch ^ jtr_sw<D>(row)) + within,
+                            base + (row + 8) * ROWB + 16 * (ch ^ jtr_sw<D>(row + 8)) + within));
 }
 
-template <int D>
-__global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(
-    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
-    const __bf16* __restrict__ tq, const __bf16* __restrict__ tk, const __bf16* __restrict__ tv,
-    float* __restrict__ out, float* __restrict__ tout, float* __restrict__ lse, int BH, int Sq, int Sk,
-    float qks, float sm) {
-  using C = JvpCfg<D>;
+// Operand images: [0] = hi (the bf16 operand itself in the bf16 mode), [1] = lo (X3 only).
+struct JvpArgs {
+  const __bf16* q[2];
+  const __bf16* k[2];
+  const __bf16* v[2];
+  const __bf16* tq[2];
+  const __bf16* tk[2];
+  const __bf16* tv[2];
+  float* out;
+  float* tout;
+  float* lse;
+  int BH, Sq, Sk;
+  float qks, sm;
+};
+
+template <int D, bool X3>
+__global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
+  using C = JvpCfg<D, X3>;
+  constexpr int NI = C::NIMG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Sq = a.Sq, Sk = a.Sk;
+  const float qks = a.qks, sm = a.sm;
   const int nq = (Sq + 127) / 128;
   int bh, qt;
-  xcd_remap(blockIdx.x, nq, BH, bh, qt);
+  xcd_remap(blockIdx.x, nq, a.BH, bh, qt);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
   const int q0 = qt * 128 + wave * 32;
   const bool active = q0 < Sq;
   const int qi = q0 + c32;
-  v8bf qf[C::NKS], tqf[C::NKS];
+  v8bf qf[NI][C::NKS], tqf[NI][C::NKS];
   if (active) {
     const long r = (long)bh * Sq + qi;
 #pragma unroll
-    for (int s = 0; s < C::NKS; ++s) {
-      qf[s] = *reinterpret_cast<const v8bf*>(q + r * D + 16 * s + 8 * h);
-      tqf[s] = *reinterpret_cast<const v8bf*>(tq + r * D + 16 * s + 8 * h);
-    }
+    for (int x = 0; x < NI; ++x)
+#pragma unroll
+      for (int s = 0; s < C::NKS; ++s) {
+        qf[x][s] = *reinterpret_cast<const v8bf*>(a.q[x] + r * D + 16 * s + 8 * h);
+        tqf[x][s] = *reinterpret_cast<const v8bf*>(a.tq[x] + r * D + 16 * s + 8 * h);
+      }
   }
   v16f o[C::NDB], ab[C::NDB];
 #pragma unroll
@@ -89,18 +111,28 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(
   float m = -INFINITY, l = 0.f, racc = 0.f;   // jvp:130-134
 
   const long kv0 = (long)bh * Sk * D;
-  const char* gk = reinterpret_cast<const char*>(k + kv0);
-  const char* gtk = reinterpret_cast<const char*>(tk + kv0);
-  const char* gv = reinterpret_cast<const char*>(v + kv0);
-  const char* gtv = reinterpret_cast<const char*>(tv + kv0);
   const int nkb = Sk / C::KB;
+  // stage layout: [K x NI][tK x NI][V x NI][tV x NI]
   auto stage = [&](int kb, int buf) {
     char* base = smem + buf * C::STAGE;
     const long off = (long)kb * C::TILE;
-    dma_tile<D, false>(gk + off, base, wave, lane);
-    dma_tile<D, false>(gtk + off, base + C::TILE, wave, lane);
-    dma_tile<D, true>(gv + off, base + 2 * C::TILE, wave, lane);
-    dma_tile<D, true>(gtv + off, base + 3 * C::TILE, wave, lane);
+#pragma unroll
+    for (int x = 0; x < NI; ++x) {
+      dma_tile<D, X3, false>(reinterpret_cast<const char*>(a.k[x] + kv0) + off, base + (0 * NI + x) * C::TILE, wave, lane);
+      dma_tile<D, X3, false>(reinterpret_cast<const char*>(a.tk[x] + kv0) + off, base + (1 * NI + x) * C::TILE, wave, lane);
+      dma_tile<D, X3, true>(reinterpret_cast<const char*>(a.v[x] + kv0) + off, base + (2 * NI + x) * C::TILE, wave, lane);
+      dma_tile<D, X3, true>(reinterpret_cast<const char*>(a.tv[x] + kv0) + off, base + (3 * NI + x) * C::TILE, wave, lane);
+    }
+  };
+  // hi*hi (+ hi*lo + lo*hi + lo*lo in X3): acc += A.B for split operands
+  auto mm = [&](const v8bf* A, const v8bf* B, v16f acc) -> v16f {
+    acc = mfma_bf16(A[0], B[0], acc);
+    if constexpr (X3) {
+      acc = mfma_bf16(A[0], B[1], acc);
+      acc = mfma_bf16(A[1], B[0], acc);
+      acc = mfma_bf16(A[1], B[1], acc);
+    }
+    return acc;
   };
   stage(0, 0);
   vmem_drain();
@@ -108,22 +140,25 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(
   for (int kb = 0; kb < nkb; ++kb) {
     if (kb + 1 < nkb) stage(kb + 1, (kb + 1) & 1);
     const char* base = smem + (kb & 1) * C::STAGE;
-    const char* kl = base;
-    const char* tkl = base + C::TILE;
-    const char* vl = base + 2 * C::TILE;
-    const char* tvl = base + 3 * C::TILE;
     if (active) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < C::KB / 32; ++u) {
         v16f sacc = v16f{}, tacc = v16f{};
 #pragma unroll
         for (int s = 0; s < C::NKS; ++s) {
           const int row = 32 * u + c32, ch = 2 * s + h;
-          const v8bf ka = *reinterpret_cast<const v8bf*>(kl + row * C::ROWB + 16 * (ch ^ jrow_sw<D>(row)));
-          const v8bf tka = *reinterpret_cast<const v8bf*>(tkl + row * C::ROWB + 16 * (ch ^ jrow_sw<D>(row)));
-          sacc = mfma_bf16(ka, qf[s], sacc);
-          tacc = mfma_bf16(ka, tqf[s], tacc);
-          tacc = mfma_bf16(tka, qf[s], tacc);
+          const int off = row * C::ROWB + 16 * (ch ^ jrow_sw<D>(row));
+          v8bf ka[NI], tka[NI], qq[NI], tqq[NI];
+#pragma unroll
+          for (int x = 0; x < NI; ++x) {
+            ka[x] = *reinterpret_cast<const v8bf*>(base + (0 * NI + x) * C::TILE + off);
+            tka[x] = *reinterpret_cast<const v8bf*>(base + (1 * NI + x) * C::TILE + off);
+            qq[x] = qf[x][s];
+            tqq[x] = tqf[x][s];
+          }
+          sacc = mm(ka, qq, sacc);        // S^T = K q^T
+          tacc = mm(ka, tqq, tacc);       // tS^T = K tq^T + tK q^T   (jvp:148-153)
+          tacc = mm(tka, qq, tacc);
         }
         float rl = -INFINITY;
 #pragma unroll
@@ -148,27 +183,40 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(
 #pragma unroll
           for (int b = 0; b < C::NDB; ++b) { o[b] *= rs; ab[b] *= rs; }
         }
-        v8bf pb[2], hb[2];
+        v8bf pb[2][NI], hb[2][NI];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          v4u pp, hp;
+          v4u pp[NI], hp[NI];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            pp[j] = pk_bf16(p[8 * s + 2 * j], p[8 * s + 2 * j + 1]);
-            hp[j] = pk_bf16(hh[8 * s + 2 * j], hh[8 * s + 2 * j + 1]);
+            const float p0 = p[8 * s + 2 * j], p1 = p[8 * s + 2 * j + 1];
+            const float h0 = hh[8 * s + 2 * j], h1 = hh[8 * s + 2 * j + 1];
+            pp[0][j] = pk_bf16(p0, p1);
+            hp[0][j] = pk_bf16(h0, h1);
+            if constexpr (X3) {
+              pp[1][j] = pk_bf16(p0 - __uint_as_float(pp[0][j] << 16), p1 - __uint_as_float(pp[0][j] & 0xffff0000u));
+              hp[1][j] = pk_bf16(h0 - __uint_as_float(hp[0][j] << 16), h1 - __uint_as_float(hp[0][j] & 0xffff0000u));
+            }
           }
-          pb[s] = __builtin_bit_cast(v8bf, pp);
-          hb[s] = __builtin_bit_cast(v8bf, hp);
+#pragma unroll
+          for (int x = 0; x < NI; ++x) {
+            pb[s][x] = __builtin_bit_cast(v8bf, pp[x]);
+            hb[s][x] = __builtin_bit_cast(v8bf, hp[x]);
+          }
         }
 #pragma unroll
         for (int b = 0; b < C::NDB; ++b) {
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const v8bf va = jtr_frag<D>(vl, 32 * u + 16 * s, b, lane);
-            const v8bf tva = jtr_frag<D>(tvl, 32 * u + 16 * s, b, lane);
-            o[b] = mfma_bf16(va, pb[s], o[b]);      // jvp:171
-            ab[b] = mfma_bf16(tva, pb[s], ab[b]);   // jvp:173-174
-            ab[b] = mfma_bf16(va, hb[s], ab[b]);    // jvp:180-181
+            v8bf va[NI], tva[NI];
+#pragma unroll
+            for (int x = 0; x < NI; ++x) {
+              va[x] = jtr_frag<D>(base + (2 * NI + x) * C::TILE, 32 * u + 16 * s, b, lane);
+              tva[x] = jtr_frag<D>(base + (3 * NI + x) * C::TILE, 32 * u + 16 * s, b, lane);
+            }
+            o[b] = mm(va, pb[s], o[b]);      // jvp:171
+            ab[b] = mm(tva, pb[s], ab[b]);   // jvp:173-174
+            ab[b] = mm(va, hb[s], ab[b]);    // jvp:180-181
           }
         }
       }
@@ -177,7 +225,7 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(
   }
   if (!active) return;
   const long r = (long)bh * Sq + qi;
-  if (h == 0) lse[r] = m + log2_f32(l);          // jvp:183
+  if (h == 0) a.lse[r] = m + log2_f32(l);          // jvp:183
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) {
 #pragma unroll
@@ -189,34 +237,86 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(
         wo[j] = of;
         wt[j] = (ab[b][4 * g + j] - racc * of) / l;             // jvp:190
       }
-      *reinterpret_cast<v4f*>(out + r * D + 32 * b + 8 * g + 4 * h) = wo;
-      *reinterpret_cast<v4f*>(tout + r * D + 32 * b + 8 * g + 4 * h) = wt;
+      *reinterpret_cast<v4f*>(a.out + r * D + 32 * b + 8 * g + 4 * h) = wo;
+      *reinterpret_cast<v4f*>(a.tout + r * D + 32 * b + 8 * g + 4 * h) = wt;
     }
   }
+}
+
+// hi = bf16(x), lo = bf16(x - hi)  (RNE both), n elements, n % 4 == 0
+__global__ void split_bf16_kernel(const float* __restrict__ x, __bf16* __restrict__ hi,
+                                  __bf16* __restrict__ lo, long n4) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const v4f v = reinterpret_cast<const v4f*>(x)[i];
+  const unsigned h01 = pk_bf16(v[0], v[1]), h23 = pk_bf16(v[2], v[3]);
+  const unsigned l01 = pk_bf16(v[0] - __uint_as_float(h01 << 16), v[1] - __uint_as_float(h01 & 0xffff0000u));
+  const unsigned l23 = pk_bf16(v[2] - __uint_as_float(h23 << 16), v[3] - __uint_as_float(h23 & 0xffff0000u));
+  reinterpret_cast<v2u*>(hi)[i] = v2u{h01, h23};
+  reinterpret_cast<v2u*>(lo)[i] = v2u{l01, l23};
 }
 
 }  // namespace qattn
 
 using namespace qattn;
 
+template <int D, bool X3>
+static int launch_jvp(const JvpArgs& a, long bh, long sq, hipStream_t st) {
+  constexpr int lds = 2 * JvpCfg<D, X3>::STAGE;
+  hipFuncSetAttribute((const void*)jvp_fwd_kernel<D, X3>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  const int nq = (int)((sq + 127) / 128);
+  hipLaunchKernelGGL((jvp_fwd_kernel<D, X3>), dim3((unsigned)(nq * bh)), dim3(256), lds, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+static JvpArgs jvp_args(const void* const* img, void* out, void* tout, void* lse, long bh, long sq,
+                        long sk, float qks, float sm, int nimg) {
+  JvpArgs a;
+  const __bf16** dst[6] = {a.q, a.k, a.v, a.tq, a.tk, a.tv};
+  for (int t = 0; t < 6; ++t) {
+    dst[t][0] = (const __bf16*)img[nimg * t];
+    dst[t][1] = (const __bf16*)img[nimg * t + nimg - 1];
+  }
+  a.out = (float*)out;
+  a.tout = (float*)tout;
+  a.lse = (float*)lse;
+  a.BH = (int)bh;
+  a.Sq = (int)sq;
+  a.Sk = (int)sk;
+  a.qks = qks;
+  a.sm = sm;
+  return a;
+}
+
 extern "C" int qattn_jvp_fwd(const void* q, const void* k, const void* v, const void* tq, const void* tk,
                              const void* tv, void* out, void* tout, void* lse, long bh, long sq, long sk,
                              int head_dim, int flags, float qks, float sm, void* stream) {
   if (flags != 0 || sq % 32 != 0 || sk % 64 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
   if (bh == 0 || sq == 0) return 0;
-  const int nq = (int)((sq + 127) / 128);
+  const void* img[6] = {q, k, v, tq, tk, tv};
+  const JvpArgs a = jvp_args(img, out, tout, lse, bh, sq, sk, qks, sm, 1);
   hipStream_t st = (hipStream_t)stream;
-#define QA_LAUNCH(Dv)                                                                              \
-  {                                                                                                \
-    constexpr int lds = 2 * JvpCfg<Dv>::STAGE;                                                     \
-    hipFuncSetAttribute((const void*)jvp_fwd_kernel<Dv>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                        lds);                                                                      \
-    hipLaunchKernelGGL((jvp_fwd_kernel<Dv>), dim3((unsigned)(nq * bh)), dim3(256), lds, st,        \
-                       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)tq,    \
-                       (const __bf16*)tk, (const __bf16*)tv, (float*)out, (float*)tout,            \
-                       (float*)lse, (int)bh, (int)sq, (int)sk, qks, sm);                           \
-  }
-  if (head_dim == 128) QA_LAUNCH(128) else QA_LAUNCH(64)
-#undef QA_LAUNCH
+  return head_dim == 128 ? launch_jvp<128, false>(a, bh, sq, st) : launch_jvp<64, false>(a, bh, sq, st);
+}
+
+extern "C" int qattn_jvp_fwd_x3(const void* q_hi, const void* q_lo, const void* k_hi, const void* k_lo,
+                                const void* v_hi, const void* v_lo, const void* tq_hi, const void* tq_lo,
+                                const void* tk_hi, const void* tk_lo, const void* tv_hi, const void* tv_lo,
+                                void* out, void* tout, void* lse, long bh, long sq, long sk, int head_dim,
+                                float qks, float sm, void* stream) {
+  if (sq % 32 != 0 || sk % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  if (bh == 0 || sq == 0) return 0;
+  const void* img[12] = {q_hi, q_lo, k_hi, k_lo, v_hi, v_lo, tq_hi, tq_lo, tk_hi, tk_lo, tv_hi, tv_lo};
+  const JvpArgs a = jvp_args(img, out, tout, lse, bh, sq, sk, qks, sm, 2);
+  hipStream_t st = (hipStream_t)stream;
+  return head_dim == 128 ? launch_jvp<128, true>(a, bh, sq, st) : launch_jvp<64, true>(a, bh, sq, st);
+}
+
+extern "C" int qattn_split_bf16(const void* x, void* hi, void* lo, long n, void* stream) {
+  if (n % 4 != 0) return 1;
+  if (n == 0) return 0;
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(split_bf16_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)x, (__bf16*)hi, (__bf16*)lo, n4);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -30,3 +30,58 @@ def test_jvp_matches_torch_func_jvp(lib, shape, ones):
     assert (tO.cpu() - tOt).abs().max().item() <= 1e-2 * max(1.0, tOt.abs().max().item() / 10)
     Or, tOr, lser = R.jvp_fwd(q, k, v, tq, tk, tv)
     assert (lse.cpu() - lser).abs().max().item() <= 1e-2
+
+
+@pytest.mark.parametrize("shape", [(1, 2, 128, 64), (2, 2, 256, 128), (1, 3, 96, 128)])
+def test_jvp_fp32_mode(lib, shape):
+    """fp32 inputs run the split-bf16 (hi*hi + hi*lo + lo*hi + lo*lo) kernel: SURVEY §8c fp32 mode, <= 1e-5
+    vs torch.func.jvp of the fp32 baseline (tO relative to its magnitude)."""
+    from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp32
+    g = torch.Generator().manual_seed(11)
+    q, k, v, tq, tk, tv = (torch.randn(shape, generator=g) for _ in range(6))
+    O, tO, lse = helion_attention_jvp_forward_fp32(*(t.cuda() for t in (q, k, v, tq, tk, tv)))
+    torch.cuda.synchronize()
+    Ot, tOt = R.jvp_truth(q, k, v, tq, tk, tv)
+    assert (O.cpu() - Ot).abs().max().item() <= 1e-5
+    assert (tO.cpu() - tOt).abs().max().item() <= 1e-5 * max(1.0, tOt.abs().max().item())
+    _, _, lser = R.jvp_fwd(q, k, v, tq, tk, tv)
+    assert (lse.cpu() - lser).abs().max().item() <= 1e-5 * max(1.0, lser.abs().max().item())
+
+
+def test_split_bf16_exact(lib):
+    from quantizedattention_amd import _lib
+    x = torch.randn(4096, generator=torch.Generator().manual_seed(3)).cuda()
+    hi = torch.empty(4096, dtype=torch.bfloat16, device="cuda")
+    lo = torch.empty_like(hi)
+    _lib.call("qattn_split_bf16", _lib.ptr(x), _lib.ptr(hi), _lib.ptr(lo), 4096, _lib.stream_of(x))
+    torch.cuda.synchronize()
+    hr = x.cpu().bfloat16()
+    lr = (x.cpu() - hr.float()).bfloat16()
+    assert torch.equal(hi.cpu().view(torch.int16), hr.view(torch.int16))
+    assert torch.equal(lo.cpu().view(torch.int16), lr.view(torch.int16))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_jvp_autograd_function_forward_mode(lib, dtype):
+    """torch.func.jvp and forward_ad dual tensors route to the HIP tangent kernel."""
+    import torch.autograd.forward_ad as fwAD
+    from quantizedattention_amd.attention_jvp import attention_jvp, helion_attention_jvp_forward_fp32
+    g = torch.Generator().manual_seed(5)
+    shape = (1, 2, 128, 64)
+    q, k, v, tq, tk, tv = (torch.randn(shape, generator=g).to(dtype).cuda() for _ in range(6))
+    O_ref, tO_ref, _ = helion_attention_jvp_forward_fp32(q, k, v, tq, tk, tv)
+    O, tO = torch.func.jvp(attention_jvp, (q, k, v), (tq, tk, tv))
+    torch.cuda.synchronize()
+    assert torch.equal(O, O_ref) and torch.equal(tO, tO_ref)
+    with fwAD.dual_level():
+        dq = fwAD.make_dual(q, tq)
+        dk = fwAD.make_dual(k, tk)
+        dv = fwAD.make_dual(v, tv)
+        out = attention_jvp(dq, dk, dv)
+        p, t = fwAD.unpack_dual(out)
+    assert torch.equal(p, O_ref) and torch.equal(t, tO_ref)
+    # matches forward-mode AD of the fp32 baseline within the mode's tolerance
+    Ot, tOt = R.jvp_truth(*(x.float().cpu() for x in (q, k, v, tq, tk, tv)))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert (O.cpu() - Ot).abs().max().item() <= tol
+    assert (tO.cpu() - tOt).abs().max().item() <= tol * max(1.0, tOt.abs().max().item())

@@ -13,7 +13,7 @@ _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
 res = {}
 for rnd in range(3):
-    for ab in (0, 1, 2, 3, 4, 5):
+    for ab in (0, 1, 2, 3, 4, 5, 6, 7):
         f = lambda: _lib.call("qattn_int8_attn_fwd_ablate", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse), B * H, S, qks, ab, st)
         for _ in range(2): f()
         torch.cuda.synchronize()
@@ -23,4 +23,5 @@ for rnd in range(3):
         b.record(); torch.cuda.synchronize()
         res.setdefault(ab, []).append(a.elapsed_time(b) / 10 * 1e3)
 for ab, t in res.items():
-    print(f"AB={ab} ({['full','no-softmax','no-PV','no-QK','no-stream','no-stream+no-softmax'][ab]}): {min(t):.1f} us")
+    names = ['full', 'no-softmax', 'no-PV', 'no-QK', 'no-stream', 'no-stream+no-softmax', 'no-softmax+halfV', 'no-softmax+halfK']
+    print(f"AB={ab} ({names[ab]}): {min(t):.1f} us")
