@@ -108,17 +108,22 @@ int qattn_int8_bwd_dq(const void* dO_i8, const void* sdO, const void* q_i8, cons
 int qattn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
                    long sq, long sk, int head_dim, int causal, float qks, void* stream);
 
-/* Backward prologue: dO f32 -> dO_bf bf16 [rows, D] and Drow f32 [rows] = rowsum(dO*O)
- * (attention_bf16.py:416, computed once per row instead of per tile). */
-int qattn_bf16_bwd_prep(const void* dO, const void* O, void* dO_bf, void* Drow, long bh, long seq,
-                        int head_dim, void* stream);
+/* Backward prologue, one pass: dO f32 -> dO_bf bf16 [rows, D] and LD f32x2 [rows] =
+ * {lse[row], D = rowsum(dO*O)} (attention_bf16.py:416, computed once per row instead of per tile). */
+int qattn_bf16_bwd_prep(const void* dO, const void* O, const void* lse, void* dO_bf, void* LD, long bh,
+                        long seq, int head_dim, void* stream);
+
+/* y = bf16(x) (round to nearest even) for n fp16 elements, n % 8 == 0: the transposed-read images of
+ * q (dK product) and k (dQ product) of qattn_bf16_bwd (no reference counterpart). */
+int qattn_f16_to_bf16(const void* x, void* y, long n, void* stream);
 
 /* Corrected FA2 backward (helion_flash_atten_2_algo_4_bwd, attention_bf16.py:299-448 with SURVEY F3
- * fixed: dS = P*(dP - D), sm_scale, deterministic dq).  q, k f16; v bf16; dO_bf bf16; lse, Drow f32;
- * out dq [bh*sq, D], dk, dv [bh*sk, D] f32.  sq % 32 == 0, sk % 64 == 0. */
-int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf, const void* lse,
-                   const void* Drow, void* dq, void* dk, void* dv, long bh, long sq, long sk,
-                   int head_dim, int causal, float qks, float sms, void* stream);
+ * fixed: dS = P*(dP - D), sm_scale, deterministic dq).  q, k f16; v bf16; dO_bf, LD from
+ * qattn_bf16_bwd_prep; q_bf, k_bf = qattn_f16_to_bf16 images of q, k.  Out dq [bh*sq, D], dk, dv
+ * [bh*sk, D] f32.  Launches one dV, one dK and one dQ kernel.  sq % 32 == 0, sk % 32 == 0. */
+int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
+                   const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh, long sq,
+                   long sk, int head_dim, int causal, float qks, float sms, void* stream);
 
 /* ---------------------------------------------------------------- JVP (attention_jvp.py) */
 

@@ -95,16 +95,20 @@ def helion_flash_atten_2_algo_4_bwd(
     dev = q.device
     st = _lib.stream_of(q)
     dO_bf = torch.empty((B, H, S, D), dtype=torch.bfloat16, device=dev)
-    Drow = torch.empty((B * H, S), dtype=torch.float32, device=dev)
-    _lib.call("qattn_bf16_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(dO_bf), _lib.ptr(Drow),
-              B * H, S, D, st)
+    LD = torch.empty((B * H, S, 2), dtype=torch.float32, device=dev)
+    _lib.call("qattn_bf16_bwd_prep", _lib.ptr(dO), _lib.ptr(O), _lib.ptr(lse), _lib.ptr(dO_bf),
+              _lib.ptr(LD), B * H, S, D, st)
+    q_bf = torch.empty(q.shape, dtype=torch.bfloat16, device=dev)
+    k_bf = torch.empty(k.shape, dtype=torch.bfloat16, device=dev)
+    _lib.call("qattn_f16_to_bf16", _lib.ptr(q), _lib.ptr(q_bf), q.numel(), st)
+    _lib.call("qattn_f16_to_bf16", _lib.ptr(k), _lib.ptr(k_bf), k.numel(), st)
     dq = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
     dk = torch.empty((B, H, Sk, D), dtype=torch.float32, device=dev)
     dv = torch.empty((B, H, Sk, D), dtype=torch.float32, device=dev)
     qks = _f32(1.0 / math.sqrt(D) * 1.44269504)
     sms = _f32(1.0 / math.sqrt(D))
-    _lib.call("qattn_bf16_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(lse),
-              _lib.ptr(Drow), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
+    _lib.call("qattn_bf16_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(LD),
+              _lib.ptr(q_bf), _lib.ptr(k_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
               B * H, S, Sk, D, int(bool(causal)), qks, sms, st)
     return dq, dk, dv
 

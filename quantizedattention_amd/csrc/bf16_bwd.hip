@@ -6,9 +6,9 @@
 //   dS = P * (dP - D)                (reference: S * (dP - D), F3)                       bf16:421
 //   dQ = sm_scale * dS K ;  dK = sm_scale * dS^T Q   (reference: qk_scale, racy dq RMW)   bf16:427-441
 //
-// Deterministic by construction: kernel A owns a block of keys and accumulates dK, dV over all
-// query tiles in registers; kernel B owns a block of queries and accumulates dQ over all key tiles
-// (S and dP are recomputed there; no atomics, no read-modify-write of global memory).
+// Deterministic by construction: each output row block has one owner workgroup that accumulates it
+// in registers over all tiles of the other side (S and dP are recomputed per kernel; no atomics, no
+// read-modify-write of global memory).
 //
 // MFMA precisions: S = Q K^T in fp16 (inputs are fp16, products exact, fp32 accumulate);
 // dP, dV, dK, dQ in bf16 (dO, dS rounded to bf16; Q/K rounded to bf16 for the dK/dQ products;
@@ -19,12 +19,15 @@
 namespace qattn {
 
 // ------------------------------------------------------------------------------------------ prep
-// D[row] = sum_d dO*O (fp32);  dO_bf16 = bf16(dO).   16 lanes per row, 8 floats per lane (D=128).
+// One pass over dO (fp32) and O: dO_bf = bf16(dO) (the dP / dV operand image) and
+// LD[row] = {lse[row], D = rowsum(dO * O)} (bf16:416, once per row instead of per tile), interleaved
+// so one 256-B LDS-DMA per 32-row tile brings both.  16 lanes per row, 8 floats per lane (D=128).
 template <int D>
 __global__ __launch_bounds__(256) void bf16_bwd_prep_kernel(const float* __restrict__ dO,
                                                             const float* __restrict__ O,
+                                                            const float* __restrict__ lse,
                                                             __bf16* __restrict__ dO_bf,
-                                                            float* __restrict__ Drow, long rows) {
+                                                            float2* __restrict__ LD, long rows) {
   constexpr int LPR = D / 8;  // lanes per row
   const long row = ((long)blockIdx.x * 256 + threadIdx.x) / LPR;
   const int c = (threadIdx.x % LPR) * 8;
@@ -40,374 +43,268 @@ __global__ __launch_bounds__(256) void bf16_bwd_prep_kernel(const float* __restr
   }
 #pragma unroll
   for (int o = LPR / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-  if (row < rows && (threadIdx.x % LPR) == 0) Drow[row] = acc;
+  if (row < rows && (threadIdx.x % LPR) == 0) LD[row] = float2{lse[row], acc};
 }
 
-template <int D>
-struct BwdCfg {
-  static constexpr int ROWB = 2 * D;     // bytes per 16-bit row
+// y = bf16(x) (RNE) for fp16 x: the transposed-read images of q (dK product) and k (dQ product)
+__global__ __launch_bounds__(256) void f16_to_bf16_kernel(const _Float16* __restrict__ x,
+                                                          __bf16* __restrict__ y, long n8) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const v8h a = reinterpret_cast<const v8h*>(x)[i];
+  v4u w;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = pk_bf16((float)a[2 * j], (float)a[2 * j + 1]);
+  reinterpret_cast<v4u*>(y)[i] = w;
+}
+
+// ------------------------------------------------------------- dV, dK, dQ: one kernel template
+// A wave owns 32 rows of one side X whose fragments stay in registers (B operands) and streams
+// 32-row tiles of the other side Y through an LDS ring filled by buffer LDS-DMA:
+//   ROLE_DV: X = K (fp16)           Y = {Q fp16 rows, dO bf16 tr image, LD}   S -> P -> dV += dO^T P
+//   ROLE_DK: X = K (fp16), V (bf16) Y = {Q fp16 rows, dO bf16 rows, Q bf16 tr image, LD}
+//                                                                           S, dP -> dS -> dK += Q^T dS
+//   ROLE_DQ: X = Q (fp16), dO (bf16) Y = {K fp16 rows, V bf16 rows, K bf16 tr image}
+//                                                                           S, dP -> dS -> dQ += K^T dS^T
+// S = Q K^T on the fp16 MFMA (exact products, fp32 accumulation), dP on the bf16 MFMA (dO, V bf16),
+// P = exp2(S*qks - lse) and dS = P*(dP - D) in fp32, then bf16 operands of the accumulating bf16
+// MFMA against the transposed (ds_read_b64_tr_b16) image of the third operand.  Software pipelined by
+// one tile: the products of tile t+1 are issued before the accumulation of tile t, and the fp32
+// P / dS of tile t+1 are computed beside its MFMAs.  Split into three kernels (S recomputed in each)
+// so that each keeps one fp32 accumulator: 2 waves per SIMD instead of 1 for a fused dK+dV.
+enum B16Role { B16_DV = 0, B16_DK = 1, B16_DQ = 2 };
+
+template <int D, int ROLE>
+struct B16Cfg {
+  static constexpr int ROWB = 2 * D;
   static constexpr int NCH = ROWB / 16;
-  static constexpr int NKS = D / 16;     // 32x32x16 k-steps over D
+  static constexpr int T16 = 32 * ROWB;                     // one 32-row 16-bit tile
+  static constexpr bool TWO = ROLE != B16_DV;               // S and dP
+  static constexpr bool HAS_LD = ROLE != B16_DQ;            // {lse, D} per row of the streamed side
+  static constexpr int NREG = TWO ? 3 : 2;                  // 16-bit regions per slot
+  static constexpr int YA = 0, YB = T16, TR = (NREG - 1) * T16, LDO = NREG * T16;
+  static constexpr int SLOT = NREG * T16 + (HAS_LD ? 256 : 0);
+  static constexpr int NSLOT = TWO ? 3 : 4;
+  static constexpr int WAVES = 4;
+  static constexpr int XROWS = 32 * WAVES;
+  static constexpr int NP = T16 / 1024;                     // 1-KiB LDS-DMA pieces per region
+  static constexpr int INST = NREG * NP;
+  static constexpr int IPW16 = INST / WAVES;
+  static constexpr int IPW = IPW16 + (HAS_LD ? 1 : 0);      // VMEM ops per wave per tile
+  static constexpr int NKS = D / 16;
   static constexpr int NDB = D / 32;
+  static constexpr int STAGE = WAVES * RowTile<D, float>::BYTES;
+  static constexpr int LDS = (NSLOT * SLOT > STAGE) ? NSLOT * SLOT : STAGE;
+  static_assert(INST % WAVES == 0, "DMA pieces split evenly over the waves");
 };
-// One LDS image serves row reads (ds_read_b128) and transposed reads (ds_read_b64_tr_b16) of the
-// same tile; the 16-B chunk swizzle is conflict-free for both (bank model of MI355X_MICROARCH §LDS):
-//   D=128 (256-B rows): ch ^ (((row&3)<<2) | ((row>>2)&3))      (cdna_hip_programming.md T10 (b))
-//   D=64  (128-B rows): ch ^ (((row&3)<<1) ^ ((row>>2)&3))
 template <int D>
-QA_DEVICE int img_off(int row, int ch) {
-  using C = BwdCfg<D>;
-  const int sw = (D == 128) ? (((row & 3) << 2) | ((row >> 2) & 3))
-                            : ((((row & 3) << 1) ^ ((row >> 2) & 3)) & 7);
-  return row * C::ROWB + 16 * (ch ^ sw);
-}
-// A operand (X^T, 32 d x 16 rows) of a 32x32x16 product from a row-major [row][d] tile.
+QA_DEVICE int b16_rsw(int row) { return (D == 128) ? (row & 15) : ((row >> 1) & 7); }   // row reads
 template <int D>
-QA_DEVICE v8s tr_frag(const char* base, int row_base, int b, int lane) {
-  const int h = lane >> 5, gg = (lane >> 4) & 1, i16 = lane & 15;
-  const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
-  const int row = row_base + 4 * h + (i16 >> 2);
-  const int ch = d / 8, within = (d % 8) * 2;
-  return ds_read_tr16_x2(base + img_off<D>(row, ch) + within, base + img_off<D>(row + 8, ch) + within);
-}
+QA_DEVICE int b16_tsw(int row) { return (row & 3) << ((D == 128) ? 2 : 1); }            // tr reads
 
-// ------------------------------------------------------------------------- kernel A: dK, dV
-// Workgroup = 4 waves x 32 keys (128 keys of one head); loops over 32-row query tiles staged in
-// LDS: Q fp16 (row image for S), Q bf16 (tr image for dK), dO bf16 (row image for dP, tr image for
-// dV), lse and D.  Orientation: query rows in registers, key on the lane.
-template <int D>
-__global__ __launch_bounds__(256, 1) void bf16_bwd_dkdv_kernel(
-    const _Float16* __restrict__ q, const _Float16* __restrict__ k, const __bf16* __restrict__ v,
-    const __bf16* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ Drow,
-    float* __restrict__ dk, float* __restrict__ dv, int BH, int Sq, int Sk, int causal, float qks,
-    float sms) {
-  using C = BwdCfg<D>;
-  constexpr int TQ = 32 * C::ROWB;           // one 32-row 16-bit tile
-  constexpr int STAGE = 3 * TQ + 2 * 32 * 4; // Qh, Qb, dO, lse, D
+template <int D, int ROLE>
+struct B16Dma {
+  using G = B16Cfg<D, ROLE>;
+  unsigned voff[G::IPW16];
+  unsigned lds_off[G::IPW16];
+  v4u rsrc[G::IPW16];
+  v4u ld_rsrc;
+  QA_DEVICE void init(int wave, int lane, int Sy, const char* ya, const char* yb, const char* tr,
+                      const char* ld) {
+    constexpr int RPI = 64 / G::NCH;
+#pragma unroll
+    for (int i = 0; i < G::IPW16; ++i) {
+      const int p = wave + G::WAVES * i;
+      const int r = p / G::NP, q = p % G::NP;
+      const bool is_tr = r == G::NREG - 1;
+      const int row = q * RPI + lane / G::NCH, c = lane % G::NCH;
+      voff[i] = row * G::ROWB + 16 * (c ^ (is_tr ? b16_tsw<D>(row) : b16_rsw<D>(row)));
+      lds_off[i] = r * G::T16 + q * 1024;
+      rsrc[i] = make_rsrc(is_tr ? tr : (r == 0 ? ya : yb), (unsigned)Sy * G::ROWB);
+    }
+    if constexpr (G::HAS_LD) ld_rsrc = make_rsrc(ld, (unsigned)Sy * 8);
+  }
+  QA_DEVICE void issue(unsigned slot_lds, int t, int lane) const {
+#pragma unroll
+    for (int i = 0; i < G::IPW16; ++i)
+      dma16_buf(rsrc[i], voff[i], (unsigned)t * G::T16, slot_lds + lds_off[i]);
+    if constexpr (G::HAS_LD) dma4_buf(ld_rsrc, 4 * lane, (unsigned)t * 256, slot_lds + G::LDO);
+  }
+};
+
+template <int D, int ROLE>
+__global__ __launch_bounds__(256, 2) void bf16_bwd_kernel(
+    const _Float16* __restrict__ xa, const __bf16* __restrict__ xb, const _Float16* __restrict__ ya,
+    const __bf16* __restrict__ yb, const __bf16* __restrict__ ytr, const float2* __restrict__ yld,
+    const float2* __restrict__ xld, float* __restrict__ out, int BH, int Sx, int Sy, int causal,
+    float qks, float osc) {
+  using G = B16Cfg<D, ROLE>;
+  constexpr bool TWO = G::TWO;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nkb = (Sk + 127) / 128;
-  int bh, kt;
-  xcd_remap(blockIdx.x, nkb, BH, bh, kt);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const int k0 = kt * 128 + wave * 32;
-  const bool active = k0 < Sk;
-  const int key = k0 + c32;
+  const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
+  int bh, xt;
+  xcd_remap(blockIdx.x, nxb, BH, bh, xt);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int x0 = xt * G::XROWS + wave * 32;
+  const bool active = x0 < Sx;
+  const int xi = x0 + c32;                      // this lane's own row
+  const long hx = (long)bh * Sx, hy = (long)bh * Sy;
+  // tile range: causal tiles masked for the whole workgroup are skipped (they contribute
+  // exp2(-128 - lse) < 2^-120 per element)
+  int t0 = 0, t1 = Sy / 32;
+  if (causal) {
+    if (ROLE == B16_DQ) t1 = min(t1, (xt * G::XROWS + G::XROWS) / 32);   // keys >= every query
+    else t0 = min(t1, (xt * G::XROWS) / 32);                               // queries <= every key
+  }
+  const int nt = t1 - t0;
 
-  // K (fp16) and V (bf16) fragments as B operands: lane holds row `key`, d = 16s + 8h .. +8
-  v8h kf[C::NKS];
-  v8bf vf[C::NKS];
-  if (active) {
-    const _Float16* kr = k + ((long)bh * Sk + key) * D + 8 * h;
-    const __bf16* vr = v + ((long)bh * Sk + key) * D + 8 * h;
+  B16Dma<D, ROLE> dma;
+  dma.init(wave, lane, Sy, reinterpret_cast<const char*>(ya + hy * D),
+           reinterpret_cast<const char*>(yb + hy * D), reinterpret_cast<const char*>(ytr + hy * D),
+           reinterpret_cast<const char*>(yld + hy));
+  const unsigned smem_lds = lds_addr(smem);
+  if (nt > 0) {
 #pragma unroll
-    for (int s = 0; s < C::NKS; ++s) {
-      kf[s] = *reinterpret_cast<const v8h*>(kr + 16 * s);
-      vf[s] = *reinterpret_cast<const v8bf*>(vr + 16 * s);
+    for (int i = 0; i < G::NSLOT - 1; ++i) dma.issue(smem_lds + i * G::SLOT, t0 + min(i, nt - 1), lane);
+  }
+
+  // own fragments (B operands): lane holds X[xi][16s + 8h .. +8]
+  const int xr = min(xi, Sx - 1);
+  v8h xfa[G::NKS];
+  v8bf xfb[TWO ? G::NKS : 1];
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s) {
+    xfa[s] = *reinterpret_cast<const v8h*>(xa + (hx + xr) * D + 16 * s + 8 * h);
+    if constexpr (TWO) xfb[s] = *reinterpret_cast<const v8bf*>(xb + (hx + xr) * D + 16 * s + 8 * h);
+  }
+  float lsex = 0.f, Dx = 0.f;
+  if constexpr (!G::HAS_LD) {
+    const float2 v = xld[hx + xr];
+    lsex = v.x;
+    Dx = v.y;
+  }
+  // lane-constant LDS offsets: row-read A operand chunk (2s+h) of row c32; tr A operand per d block
+  int roff[G::NKS], troff[G::NDB];
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s) roff[s] = c32 * G::ROWB + 16 * ((2 * s + h) ^ b16_rsw<D>(c32));
+  {
+    const int gg = (lane >> 4) & 1, i16 = lane & 15;
+    const int row = 4 * h + (i16 >> 2);
+#pragma unroll
+    for (int b = 0; b < G::NDB; ++b) {
+      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
+      troff[b] = G::TR + row * G::ROWB + 16 * ((d / 8) ^ b16_tsw<D>(row)) + (d % 8) * 2;
     }
   }
-  v16f dka[C::NDB], dva[C::NDB];
+  v16f acc[G::NDB];
 #pragma unroll
-  for (int b = 0; b < C::NDB; ++b) { dka[b] = v16f{}; dva[b] = v16f{}; }
+  for (int b = 0; b < G::NDB; ++b) acc[b] = v16f{};
 
-  const long qrow0 = (long)bh * Sq;
-  const int nqt = Sq / 32;
-  int qt0 = 0;
-  if (causal) qt0 = min(nqt, (kt * 128) / 32);  // tiles with q_max <= k_min are fully masked
-  // staging: 3 tiles x 32 rows x NCH chunks of 16 B -> per thread (3*32*NCH)/256 chunks
-  constexpr int CH_PER_TILE = 32 * C::NCH;
-  constexpr int LOADS = (CH_PER_TILE + 255) / 256;
-  v4i sq_[LOADS], sd_[LOADS];
-  float slse = 0.f, sD = 0.f;
-  auto stage_load = [&](int t) {
-    const long r0 = qrow0 + 32L * t;
+  auto slot = [&](int t) -> const char* { return smem + ((t - t0) % G::NSLOT) * G::SLOT; };
+  // S (fp16 MFMA) and dP (bf16 MFMA) of tile t, rows = streamed side, lane = own row
+  auto products = [&](int t, v16f& sa, v16f& pa) {
+    const char* base = slot(t);
+    sa = v16f{};
+    pa = v16f{};
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int e = i * 256 + tid;
-      if (e < CH_PER_TILE) {
-        const int row = e / C::NCH, ch = e % C::NCH;
-        sq_[i] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(q + (r0 + row) * D) + 16 * ch);
-        sd_[i] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(dO + (r0 + row) * D) + 16 * ch);
-      }
+    for (int s = 0; s < G::NKS; ++s) {
+      sa = mfma_f16(*reinterpret_cast<const v8h*>(base + G::YA + roff[s]), xfa[s], sa);
+      if constexpr (TWO) pa = mfma_bf16(*reinterpret_cast<const v8bf*>(base + G::YB + roff[s]), xfb[s], pa);
     }
-    if (tid < 32) slse = lse[r0 + tid];
-    else if (tid < 64) sD = Drow[r0 + tid - 32];
   };
-  auto stage_store = [&](int buf) {
-    char* base = smem + buf * STAGE;
-    char* qh = base;
-    char* qb = base + TQ;
-    char* dd = base + 2 * TQ;
-    float* ls = reinterpret_cast<float*>(base + 3 * TQ);
-#pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int e = i * 256 + tid;
-      if (e < CH_PER_TILE) {
-        const int row = e / C::NCH, ch = e % C::NCH;
-        *reinterpret_cast<v4i*>(qh + img_off<D>(row, ch)) = sq_[i];
-        *reinterpret_cast<v4i*>(dd + img_off<D>(row, ch)) = sd_[i];
-        // fp16 -> bf16 copy of Q for the dK product
-        const v8h x = __builtin_bit_cast(v8h, sq_[i]);
-        v4u pk;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pk[j] = pk_bf16((float)x[2 * j], (float)x[2 * j + 1]);
-        *reinterpret_cast<v4u*>(qb + img_off<D>(row, ch)) = pk;
-      }
-    }
-    if (tid < 32) ls[tid] = slse;
-    else if (tid < 64) ls[tid] = sD;
-  };
-
-  if (qt0 < nqt) {
-    stage_load(qt0);
-    stage_store(0);
-  }
-  __syncthreads();
-  for (int t = qt0; t < nqt; ++t) {
-    const int buf = (t - qt0) & 1;
-    if (t + 1 < nqt) stage_load(t + 1);
-    const char* base = smem + buf * STAGE;
-    const char* qh = base;
-    const char* qb = base + TQ;
-    const char* dd = base + 2 * TQ;
-    const float* ls = reinterpret_cast<const float*>(base + 3 * TQ);
-    const int qtile0 = 32 * t;
-    const bool skip = causal && (qtile0 + 31 <= k0);  // fully masked for this wave's keys
-    if (active && !skip) {
-      // S[q][key] = Q K^T (fp16) and dP[q][key] = dO V^T (bf16); q rows in registers
-      v16f sacc = v16f{}, pacc = v16f{};
-#pragma unroll
-      for (int s = 0; s < C::NKS; ++s) {
-        const v8h a = *reinterpret_cast<const v8h*>(qh + img_off<D>(c32, 2 * s + h));
-        sacc = mfma_f16(a, kf[s], sacc);
-      }
-#pragma unroll
-      for (int s = 0; s < C::NKS; ++s) {
-        const v8bf a = *reinterpret_cast<const v8bf*>(dd + img_off<D>(c32, 2 * s + h));
-        pacc = mfma_bf16(a, vf[s], pacc);
-      }
-      // row constants for rows (r&3) + 8(r>>2) + 4h: 4 contiguous floats per group g
-      float lr[16], dr[16];
+  // fp32 P (DV) or dS (DK, DQ) of tile t
+  auto values = [&](int t, const v16f& sa, const v16f& pa, float* X) {
+    const int y0 = 32 * t;
+    const bool mask = causal && (ROLE == B16_DQ ? (y0 + 31 >= x0) : (y0 <= x0 + 31));
+    if constexpr (G::HAS_LD) {
+      const float* ld = reinterpret_cast<const float*>(slot(t) + G::LDO);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const v4f l4 = *reinterpret_cast<const v4f*>(ls + 8 * g + 4 * h);
-        const v4f d4 = *reinterpret_cast<const v4f*>(ls + 32 + 8 * g + 4 * h);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { lr[4 * g + j] = l4[j]; dr[4 * g + j] = d4[j]; }
-      }
-      const bool need_mask = causal && (qtile0 <= k0 + 31);
-      float p[16], ds[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float sc = sacc[i] * qks;
-        if (need_mask) {
-          const int qi = qtile0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (qi - key <= 0) sc = -128.0f;
-        }
-        p[i] = exp2_f32(sc - lr[i]);
-        ds[i] = p[i] * (pacc[i] - dr[i]);
-      }
-      v8bf pb[2], db[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        v4u pp, dq;
+        const v4f a = *reinterpret_cast<const v4f*>(ld + 2 * (8 * g + 4 * h));
+        const v4f b = *reinterpret_cast<const v4f*>(ld + 2 * (8 * g + 4 * h) + 4);
+        const float lse_r[4] = {a[0], a[2], b[0], b[2]};
+        const float d_r[4] = {a[1], a[3], b[1], b[3]};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          pp[j] = pk_bf16(p[8 * s + 2 * j], p[8 * s + 2 * j + 1]);
-          dq[j] = pk_bf16(ds[8 * s + 2 * j], ds[8 * s + 2 * j + 1]);
-        }
-        pb[s] = __builtin_bit_cast(v8bf, pp);
-        db[s] = __builtin_bit_cast(v8bf, dq);
-      }
-      // dV^T[d][key] += dO^T P ;  dK^T[d][key] += Q^T dS
-#pragma unroll
-      for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const v8bf ao = __builtin_bit_cast(v8bf, tr_frag<D>(dd, 16 * s, b, lane));
-          dva[b] = mfma_bf16(ao, pb[s], dva[b]);
-          const v8bf aq = __builtin_bit_cast(v8bf, tr_frag<D>(qb, 16 * s, b, lane));
-          dka[b] = mfma_bf16(aq, db[s], dka[b]);
+          const int i = 4 * g + j;
+          float sc = sa[i] * qks;                                          // bf16:376-377
+          if (mask && y0 + 8 * g + 4 * h + j - xi <= 0) sc = -128.0f;       // bf16:379-389
+          const float p = exp2_f32(sc - lse_r[j]);                         // bf16:392
+          if constexpr (ROLE == B16_DV) X[i] = p;
+          else X[i] = p * (pa[i] - d_r[j]);                                // dS = P (dP - D), F3
         }
       }
-    }
-    if (t + 1 < nqt) stage_store(buf ^ 1);
-    __syncthreads();
-  }
-  if (!active) return;
-  // write dK = sms * dK^T, dV (fp32, row-major [key][d]); lane = key, regs = d
-  const long krow = (long)bh * Sk + key;
-  float* dkr = dk + krow * D;
-  float* dvr = dv + krow * D;
+    } else {
 #pragma unroll
-  for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      v4f wk, wv;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { wk[j] = dka[b][4 * g + j] * sms; wv[j] = dva[b][4 * g + j]; }
-      *reinterpret_cast<v4f*>(dkr + 32 * b + 8 * g + 4 * h) = wk;
-      *reinterpret_cast<v4f*>(dvr + 32 * b + 8 * g + 4 * h) = wv;
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------- kernel B: dQ
-// Workgroup = 4 waves x 32 queries; loops over 64-key blocks staged in LDS: K fp16 (row image for
-// S), K bf16 (tr image for dQ), V bf16 (row image for dP).  Orientation: keys in registers, query
-// on the lane (lse, D are per-lane scalars).
-template <int D>
-__global__ __launch_bounds__(256, 1) void bf16_bwd_dq_kernel(
-    const _Float16* __restrict__ q, const _Float16* __restrict__ k, const __bf16* __restrict__ v,
-    const __bf16* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ Drow,
-    float* __restrict__ dq, int BH, int Sq, int Sk, int causal, float qks, float sms) {
-  using C = BwdCfg<D>;
-  constexpr int KB = 64;
-  constexpr int TK = KB * C::ROWB;
-  constexpr int STAGE = 3 * TK;  // Kh, Kb, V
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nqb = (Sq + 127) / 128;
-  int bh, qt;
-  xcd_remap(blockIdx.x, nqb, BH, bh, qt);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const int q0 = qt * 128 + wave * 32;
-  const bool active = q0 < Sq;
-  const int qi = q0 + c32;
-
-  v8h qf[C::NKS];
-  v8bf of[C::NKS];
-  float lq = 0.f, dq_ = 0.f;
-  if (active) {
-    const long r = (long)bh * Sq + qi;
-    const _Float16* qr = q + r * D + 8 * h;
-    const __bf16* orr = dO + r * D + 8 * h;
-#pragma unroll
-    for (int s = 0; s < C::NKS; ++s) {
-      qf[s] = *reinterpret_cast<const v8h*>(qr + 16 * s);
-      of[s] = *reinterpret_cast<const v8bf*>(orr + 16 * s);
-    }
-    lq = lse[r];
-    dq_ = Drow[r];
-  }
-  v16f acc[C::NDB];
-#pragma unroll
-  for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
-
-  int nkb = (Sk + KB - 1) / KB;
-  if (causal) nkb = min(nkb, (qt * 128 + 127 + KB - 1) / KB);  // blocks with k_min >= q_max skipped
-  constexpr int CH = KB * C::NCH;
-  constexpr int LOADS = CH / 256;
-  v4i sk_[LOADS], sv_[LOADS];
-  const char* kbase = reinterpret_cast<const char*>(k + (long)bh * Sk * D);
-  const char* vbase = reinterpret_cast<const char*>(v + (long)bh * Sk * D);
-  auto stage_load = [&](int kb) {
-#pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int e = i * 256 + tid, row = e / C::NCH, ch = e % C::NCH;
-      const long off = (long)(kb * KB + row) * C::ROWB + 16 * ch;
-      sk_[i] = *reinterpret_cast<const v4i*>(kbase + off);
-      sv_[i] = *reinterpret_cast<const v4i*>(vbase + off);
+      for (int i = 0; i < 16; ++i) {
+        float sc = sa[i] * qks;
+        if (mask && xi - (y0 + (i & 3) + 8 * (i >> 2) + 4 * h) <= 0) sc = -128.0f;
+        X[i] = exp2_f32(sc - lsex) * (pa[i] - Dx);
+      }
     }
   };
-  auto stage_store = [&](int buf) {
-    char* kh = smem + buf * STAGE;
-    char* kb_ = kh + TK;
-    char* vl = kh + 2 * TK;
+  auto operand = [&](const float* X, v8bf* op) {
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int e = i * 256 + tid, row = e / C::NCH, ch = e % C::NCH;
-      *reinterpret_cast<v4i*>(kh + img_off<D>(row, ch)) = sk_[i];
-      *reinterpret_cast<v4i*>(vl + img_off<D>(row, ch)) = sv_[i];
-      const v8h x = __builtin_bit_cast(v8h, sk_[i]);
-      v4u pk;
+    for (int s = 0; s < 2; ++s) {
+      v4u w;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pk[j] = pk_bf16((float)x[2 * j], (float)x[2 * j + 1]);
-      *reinterpret_cast<v4u*>(kb_ + img_off<D>(row, ch)) = pk;
+      for (int j = 0; j < 4; ++j) w[j] = pk_bf16(X[8 * s + 2 * j], X[8 * s + 2 * j + 1]);
+      op[s] = __builtin_bit_cast(v8bf, w);
     }
   };
-  if (nkb > 0) {
-    stage_load(0);
-    stage_store(0);
-  }
+  auto tr_load = [&](int t, v8bf* ta) {
+    const char* base = slot(t);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < G::NDB; ++b) {
+        const char* a = base + troff[b] + 16 * s * G::ROWB;
+        ta[s * G::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * G::ROWB));
+      }
+  };
+
+  vmem_drain();
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
-    if (kb + 1 < nkb) stage_load(kb + 1);
-    const char* kh = smem + (kb & 1) * STAGE;
-    const char* kbf = kh + TK;
-    const char* vl = kh + 2 * TK;
-    if (active) {
-#pragma unroll
-      for (int u = 0; u < KB / 32; ++u) {
-        const int key_t0 = kb * KB + 32 * u;
-        if (causal && key_t0 >= q0 + 31) continue;  // fully masked for this wave (uniform)
-        v16f sacc = v16f{}, pacc = v16f{};
-#pragma unroll
-        for (int s = 0; s < C::NKS; ++s) {
-          const v8h a = *reinterpret_cast<const v8h*>(kh + img_off<D>(32 * u + c32, 2 * s + h));
-          sacc = mfma_f16(a, qf[s], sacc);
-        }
-#pragma unroll
-        for (int s = 0; s < C::NKS; ++s) {
-          const v8bf a = *reinterpret_cast<const v8bf*>(vl + img_off<D>(32 * u + c32, 2 * s + h));
-          pacc = mfma_bf16(a, of[s], pacc);
-        }
-        const bool need_mask = causal && (key_t0 + 31 >= q0);
-        float ds[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float sc = sacc[i] * qks;
-          if (need_mask) {
-            const int kk = key_t0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (qi - kk <= 0) sc = -128.0f;
-          }
-          const float p = exp2_f32(sc - lq);
-          ds[i] = p * (pacc[i] - dq_);
-        }
-        v8bf db[2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          v4u pk;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pk[j] = pk_bf16(ds[8 * s + 2 * j], ds[8 * s + 2 * j + 1]);
-          db[s] = __builtin_bit_cast(v8bf, pk);
-        }
-#pragma unroll
-        for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const v8bf a = __builtin_bit_cast(v8bf, tr_frag<D>(kbf, 32 * u + 16 * s, b, lane));
-            acc[b] = mfma_bf16(a, db[s], acc[b]);
-          }
-        }
-      }
+  if (nt > 0) {
+    float X[16];
+    {
+      v16f sa, pa;
+      products(t0, sa, pa);
+      values(t0, sa, pa, X);
     }
-    if (kb + 1 < nkb) stage_store((kb + 1) & 1);
-    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+      // tile t+1 landed (later tiles may be in flight); the slot of tile t-1 is free
+      ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
+      dma.issue(smem_lds + ((t - t0 + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
+                min(t + G::NSLOT - 1, t1 - 1), lane);
+      const int tn = min(t + 1, t1 - 1);
+      v8bf ta[2 * G::NDB];
+      tr_load(t, ta);
+      v16f sa, pa;
+      products(tn, sa, pa);
+      v8bf op[2];
+      operand(X, op);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int b = 0; b < G::NDB; ++b) acc[b] = mfma_bf16(ta[s * G::NDB + b], op[s], acc[b]);
+      values(tn, sa, pa, X);
+    }
   }
+  vmcnt_wait_all();
+  __syncthreads();   // the ring becomes the output staging area
   if (!active) return;
-  float* dqr = dq + ((long)bh * Sq + qi) * D;
-#pragma unroll
-  for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      v4f w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = acc[b][4 * g + j] * sms;
-      *reinterpret_cast<v4f*>(dqr + 32 * b + 8 * g + 4 * h) = w;
-    }
-  }
-}
-
-template <typename K>
-static void set_lds(K kernel, int bytes) {
-  hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  store_rows<D, float>(acc, osc, smem + wave * RowTile<D, float>::BYTES, out + (hx + x0) * D, lane);
 }
 
 }  // namespace qattn
 
 using namespace qattn;
 
-extern "C" int qattn_bf16_bwd_prep(const void* dO, const void* O, void* dO_bf, void* Drow, long bh,
-                                   long seq, int head_dim, void* stream) {
+extern "C" int qattn_bf16_bwd_prep(const void* dO, const void* O, const void* lse, void* dO_bf,
+                                   void* LD, long bh, long seq, int head_dim, void* stream) {
   if (head_dim != 64 && head_dim != 128) return 1;
   const long rows = bh * seq;
   if (rows == 0) return 0;
@@ -416,37 +313,58 @@ extern "C" int qattn_bf16_bwd_prep(const void* dO, const void* O, void* dO_bf, v
   hipStream_t st = (hipStream_t)stream;
   if (head_dim == 128)
     hipLaunchKernelGGL((bf16_bwd_prep_kernel<128>), grid, block, 0, st, (const float*)dO,
-                       (const float*)O, (__bf16*)dO_bf, (float*)Drow, rows);
+                       (const float*)O, (const float*)lse, (__bf16*)dO_bf, (float2*)LD, rows);
   else
     hipLaunchKernelGGL((bf16_bwd_prep_kernel<64>), grid, block, 0, st, (const float*)dO,
-                       (const float*)O, (__bf16*)dO_bf, (float*)Drow, rows);
+                       (const float*)O, (const float*)lse, (__bf16*)dO_bf, (float2*)LD, rows);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+extern "C" int qattn_f16_to_bf16(const void* x, void* y, long n, void* stream) {
+  if (n % 8 != 0) return 1;
+  const long n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(f16_to_bf16_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const _Float16*)x, (__bf16*)y, n8);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+template <int D, int ROLE>
+static void launch_b16(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
+                       const void* yld, const void* xld, void* out, long bh, long sx, long sy,
+                       int causal, float qks, float osc, hipStream_t st) {
+  using G = B16Cfg<D, ROLE>;
+  hipFuncSetAttribute((const void*)bf16_bwd_kernel<D, ROLE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      G::LDS);
+  const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
+  hipLaunchKernelGGL((bf16_bwd_kernel<D, ROLE>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES), G::LDS,
+                     st, (const _Float16*)xa, (const __bf16*)xb, (const _Float16*)ya, (const __bf16*)yb,
+                     (const __bf16*)ytr, (const float2*)yld, (const float2*)xld, (float*)out, (int)bh,
+                     (int)sx, (int)sy, causal, qks, osc);
+}
+
+template <int D>
+static void bf16_bwd_d(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
+                       const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh,
+                       long sq, long sk, int causal, float qks, float sms, hipStream_t st) {
+  // dV: own K / streamed Q rows, dO tr image, LD
+  launch_b16<D, B16_DV>(k, nullptr, q, nullptr, dO_bf, LD, nullptr, dv, bh, sk, sq, causal, qks, 1.0f, st);
+  // dK: own K, V / streamed Q rows, dO rows, Q bf16 tr image, LD
+  launch_b16<D, B16_DK>(k, v, q, dO_bf, q_bf, LD, nullptr, dk, bh, sk, sq, causal, qks, sms, st);
+  // dQ: own Q, dO (+ LD of their rows) / streamed K rows, V rows, K bf16 tr image
+  launch_b16<D, B16_DQ>(q, dO_bf, k, v, k_bf, nullptr, LD, dq, bh, sq, sk, causal, qks, sms, st);
+}
+
 extern "C" int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf,
-                              const void* lse, const void* Drow, void* dq, void* dk, void* dv,
-                              long bh, long sq, long sk, int head_dim, int causal, float qks,
+                              const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
+                              void* dv, long bh, long sq, long sk, int head_dim, int causal, float qks,
                               float sms, void* stream) {
-  if (sq % 32 != 0 || sk % 64 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  if (bh == 0 || sq == 0) return 0;
+  if (sq % 32 != 0 || sk % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  if (bh == 0 || sq == 0 || sk == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int nkb = (int)((sk + 127) / 128), nqb = (int)((sq + 127) / 128);
-#define QA_LAUNCH(Dv)                                                                              \
-  {                                                                                                \
-    constexpr int sA = 2 * (3 * 32 * 2 * Dv + 256);                                                \
-    constexpr int sB = 2 * 3 * 64 * 2 * Dv;                                                        \
-    set_lds(bf16_bwd_dkdv_kernel<Dv>, sA);                                                         \
-    set_lds(bf16_bwd_dq_kernel<Dv>, sB);                                                           \
-    hipLaunchKernelGGL((bf16_bwd_dkdv_kernel<Dv>), dim3((unsigned)(nkb * bh)), dim3(256), sA, st,   \
-                       (const _Float16*)q, (const _Float16*)k, (const __bf16*)v,                     \
-                       (const __bf16*)dO_bf, (const float*)lse, (const float*)Drow, (float*)dk,      \
-                       (float*)dv, (int)bh, (int)sq, (int)sk, causal, qks, sms);                    \
-    hipLaunchKernelGGL((bf16_bwd_dq_kernel<Dv>), dim3((unsigned)(nqb * bh)), dim3(256), sB, st,     \
-                       (const _Float16*)q, (const _Float16*)k, (const __bf16*)v,                     \
-                       (const __bf16*)dO_bf, (const float*)lse, (const float*)Drow, (float*)dq,      \
-                       (int)bh, (int)sq, (int)sk, causal, qks, sms);                                 \
-  }
-  if (head_dim == 128) QA_LAUNCH(128) else QA_LAUNCH(64)
-#undef QA_LAUNCH
+  if (head_dim == 128)
+    bf16_bwd_d<128>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, causal, qks, sms, st);
+  else
+    bf16_bwd_d<64>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, causal, qks, sms, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
