@@ -31,6 +31,7 @@ CFLAGS = [
 # v_max x,x of its bit-cast inputs.
 FILE_FLAGS = {
     "bf16_fwd.hip": ["-fno-slp-vectorize", "-mno-amdgpu-ieee", "-fno-honor-nans"],
+    "bf16_bwd.hip": ["-fno-slp-vectorize"],
 }
 
 

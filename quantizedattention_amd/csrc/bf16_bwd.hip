@@ -14,6 +14,8 @@
 // dP, dV, dK, dQ in bf16 (dO, dS rounded to bf16; Q/K rounded to bf16 for the dK/dQ products;
 // V is bf16 already), fp32 accumulate.  Causal tiles that are entirely masked contribute
 // exp2(-128 - lse) < 2^-120 per element and are skipped.
+#include <type_traits>
+
 #include "common.h"
 
 namespace qattn {
@@ -73,6 +75,12 @@ __global__ __launch_bounds__(256) void f16_to_bf16_kernel(const _Float16* __rest
 // P / dS of tile t+1 are computed beside its MFMAs.  Split into three kernels (S recomputed in each)
 // so that each keeps one fp32 accumulator: 2 waves per SIMD instead of 1 for a fused dK+dV.
 enum B16Role { B16_DV = 0, B16_DK = 1, B16_DQ = 2 };
+#ifndef QA_B16_DV_OCC
+#define QA_B16_DV_OCC 2
+#endif
+#ifndef QA_B16_DV_NSLOT
+#define QA_B16_DV_NSLOT 3
+#endif
 
 template <int D, int ROLE>
 struct B16Cfg {
@@ -84,7 +92,7 @@ struct B16Cfg {
   static constexpr int NREG = TWO ? 3 : 2;                  // 16-bit regions per slot
   static constexpr int YA = 0, YB = T16, TR = (NREG - 1) * T16, LDO = NREG * T16;
   static constexpr int SLOT = NREG * T16 + (HAS_LD ? 256 : 0);
-  static constexpr int NSLOT = TWO ? 3 : 4;
+  static constexpr int NSLOT = (ROLE == B16_DV) ? QA_B16_DV_NSLOT : 3;
   static constexpr int WAVES = 4;
   static constexpr int XROWS = 32 * WAVES;
   static constexpr int NP = T16 / 1024;                     // 1-KiB LDS-DMA pieces per region
@@ -93,7 +101,7 @@ struct B16Cfg {
   static constexpr int IPW = IPW16 + (HAS_LD ? 1 : 0);      // VMEM ops per wave per tile
   static constexpr int NKS = D / 16;
   static constexpr int NDB = D / 32;
-  static constexpr int STAGE = WAVES * RowTile<D, float>::BYTES;
+  static constexpr int STAGE = WAVES * RowTile<D, float, 2>::BYTES;   // epilogue in two column halves
   static constexpr int LDS = (NSLOT * SLOT > STAGE) ? NSLOT * SLOT : STAGE;
   static_assert(INST % WAVES == 0, "DMA pieces split evenly over the waves");
 };
@@ -132,12 +140,12 @@ struct B16Dma {
   }
 };
 
-template <int D, int ROLE>
-__global__ __launch_bounds__(256, 2) void bf16_bwd_kernel(
+template <int D, int ROLE, bool CAUSAL>
+__global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void bf16_bwd_kernel(
     const _Float16* __restrict__ xa, const __bf16* __restrict__ xb, const _Float16* __restrict__ ya,
     const __bf16* __restrict__ yb, const __bf16* __restrict__ ytr, const float2* __restrict__ yld,
-    const float2* __restrict__ xld, float* __restrict__ out, int BH, int Sx, int Sy, int causal,
-    float qks, float osc) {
+    const float2* __restrict__ xld, float* __restrict__ out, int BH, int Sx, int Sy, float qks,
+    float osc) {
   using G = B16Cfg<D, ROLE>;
   constexpr bool TWO = G::TWO;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -154,7 +162,7 @@ __global__ __launch_bounds__(256, 2) void bf16_bwd_kernel(
   // tile range: causal tiles masked for the whole workgroup are skipped (they contribute
   // exp2(-128 - lse) < 2^-120 per element)
   int t0 = 0, t1 = Sy / 32;
-  if (causal) {
+  if (CAUSAL) {
     if (ROLE == B16_DQ) t1 = min(t1, (xt * G::XROWS + G::XROWS) / 32);   // keys >= every query
     else t0 = min(t1, (xt * G::XROWS) / 32);                               // queries <= every key
   }
@@ -202,10 +210,12 @@ __global__ __launch_bounds__(256, 2) void bf16_bwd_kernel(
 #pragma unroll
   for (int b = 0; b < G::NDB; ++b) acc[b] = v16f{};
 
-  auto slot = [&](int t) -> const char* { return smem + ((t - t0) % G::NSLOT) * G::SLOT; };
-  // S (fp16 MFMA) and dP (bf16 MFMA) of tile t, rows = streamed side, lane = own row
-  auto products = [&](int t, v16f& sa, v16f& pa) {
-    const char* base = slot(t);
+  // tile t lives in ring slot (t - t0) % NSLOT; the loop is unrolled by NSLOT so the slot is a
+  // compile-time constant and every LDS address a lane-constant VGPR plus an instruction offset
+  auto slot = [&](auto SLc) -> const char* { return smem + decltype(SLc)::value * G::SLOT; };
+  // S (fp16 MFMA) and dP (bf16 MFMA) of the tile in slot SL, rows = streamed side, lane = own row
+  auto products = [&](auto SLc, v16f& sa, v16f& pa) {
+    const char* base = slot(SLc);
     sa = v16f{};
     pa = v16f{};
 #pragma unroll
@@ -215,11 +225,11 @@ __global__ __launch_bounds__(256, 2) void bf16_bwd_kernel(
     }
   };
   // fp32 P (DV) or dS (DK, DQ) of tile t
-  auto values = [&](int t, const v16f& sa, const v16f& pa, float* X) {
+  auto values = [&](auto SLc, int t, const v16f& sa, const v16f& pa, float* X) {
     const int y0 = 32 * t;
-    const bool mask = causal && (ROLE == B16_DQ ? (y0 + 31 >= x0) : (y0 <= x0 + 31));
+    const bool mask = CAUSAL && (ROLE == B16_DQ ? (y0 + 31 >= x0) : (y0 <= x0 + 31));
     if constexpr (G::HAS_LD) {
-      const float* ld = reinterpret_cast<const float*>(slot(t) + G::LDO);
+      const float* ld = reinterpret_cast<const float*>(slot(SLc) + G::LDO);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const v4f a = *reinterpret_cast<const v4f*>(ld + 2 * (8 * g + 4 * h));
@@ -254,8 +264,8 @@ __global__ __launch_bounds__(256, 2) void bf16_bwd_kernel(
       op[s] = __builtin_bit_cast(v8bf, w);
     }
   };
-  auto tr_load = [&](int t, v8bf* ta) {
-    const char* base = slot(t);
+  auto tr_load = [&](auto SLc, v8bf* ta) {
+    const char* base = slot(SLc);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -267,36 +277,46 @@ __global__ __launch_bounds__(256, 2) void bf16_bwd_kernel(
 
   vmem_drain();
   __syncthreads();
+  static_assert(G::NSLOT == 3, "the tile loop below is unrolled for a 3-slot ring");
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  float X[16];
+  // one tile: slot SL holds tile t, slot NX = (SL+1)%3 tile min(t+1, t1-1) (the DMA clamps to the
+  // last tile, so the slot after the last one holds a duplicate and the loop body stays uniform)
+  auto step = [&](auto SLc, auto NXc, int t) {
+    ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();   // tile t+1 landed; the slot of tile t-1 is free
+    dma.issue(smem_lds + ((decltype(SLc)::value + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
+              min(t + G::NSLOT - 1, t1 - 1), lane);
+    const int tn = min(t + 1, t1 - 1);
+    v8bf ta[2 * G::NDB];
+    tr_load(SLc, ta);
+    v16f sa, pa;
+    products(NXc, sa, pa);
+    v8bf op[2];
+    operand(X, op);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < G::NDB; ++b) acc[b] = mfma_bf16(ta[s * G::NDB + b], op[s], acc[b]);
+    values(NXc, tn, sa, pa, X);
+  };
   if (nt > 0) {
-    float X[16];
     {
       v16f sa, pa;
-      products(t0, sa, pa);
-      values(t0, sa, pa, X);
+      products(I0{}, sa, pa);
+      values(I0{}, t0, sa, pa, X);
     }
-    for (int t = t0; t < t1; ++t) {
-      // tile t+1 landed (later tiles may be in flight); the slot of tile t-1 is free
-      ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
-      dma.issue(smem_lds + ((t - t0 + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
-                min(t + G::NSLOT - 1, t1 - 1), lane);
-      const int tn = min(t + 1, t1 - 1);
-      v8bf ta[2 * G::NDB];
-      tr_load(t, ta);
-      v16f sa, pa;
-      products(tn, sa, pa);
-      v8bf op[2];
-      operand(X, op);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int b = 0; b < G::NDB; ++b) acc[b] = mfma_bf16(ta[s * G::NDB + b], op[s], acc[b]);
-      values(tn, sa, pa, X);
+    for (int t = t0; t < t1; t += 3) {
+      step(I0{}, I1{}, t);
+      if (t + 1 < t1) step(I1{}, I2{}, t + 1);
+      if (t + 2 < t1) step(I2{}, I0{}, t + 2);
     }
   }
   vmcnt_wait_all();
   __syncthreads();   // the ring becomes the output staging area
   if (!active) return;
-  store_rows<D, float>(acc, osc, smem + wave * RowTile<D, float>::BYTES, out + (hx + x0) * D, lane);
+  store_rows<D, float, 2>(acc, osc, smem + wave * RowTile<D, float, 2>::BYTES, out + (hx + x0) * D, lane);
 }
 
 }  // namespace qattn
@@ -329,18 +349,25 @@ extern "C" int qattn_f16_to_bf16(const void* x, void* y, long n, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+template <int D, int ROLE, bool CAUSAL>
+static void launch_b16c(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
+                        const void* yld, const void* xld, void* out, long bh, long sx, long sy,
+                        float qks, float osc, hipStream_t st) {
+  using G = B16Cfg<D, ROLE>;
+  hipFuncSetAttribute((const void*)bf16_bwd_kernel<D, ROLE, CAUSAL>,
+                      hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+  const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
+  hipLaunchKernelGGL((bf16_bwd_kernel<D, ROLE, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
+                     G::LDS, st, (const _Float16*)xa, (const __bf16*)xb, (const _Float16*)ya,
+                     (const __bf16*)yb, (const __bf16*)ytr, (const float2*)yld, (const float2*)xld,
+                     (float*)out, (int)bh, (int)sx, (int)sy, qks, osc);
+}
 template <int D, int ROLE>
 static void launch_b16(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
                        const void* yld, const void* xld, void* out, long bh, long sx, long sy,
                        int causal, float qks, float osc, hipStream_t st) {
-  using G = B16Cfg<D, ROLE>;
-  hipFuncSetAttribute((const void*)bf16_bwd_kernel<D, ROLE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      G::LDS);
-  const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
-  hipLaunchKernelGGL((bf16_bwd_kernel<D, ROLE>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES), G::LDS,
-                     st, (const _Float16*)xa, (const __bf16*)xb, (const _Float16*)ya, (const __bf16*)yb,
-                     (const __bf16*)ytr, (const float2*)yld, (const float2*)xld, (float*)out, (int)bh,
-                     (int)sx, (int)sy, causal, qks, osc);
+  if (causal) launch_b16c<D, ROLE, true>(xa, xb, ya, yb, ytr, yld, xld, out, bh, sx, sy, qks, osc, st);
+  else launch_b16c<D, ROLE, false>(xa, xb, ya, yb, ytr, yld, xld, out, bh, sx, sy, qks, osc, st);
 }
 
 template <int D>

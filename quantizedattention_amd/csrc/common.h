@@ -310,41 +310,50 @@ QA_DEVICE v8s ds_read_tr16_x2(const void* addr0, const void* addr1) {
 // read back 16 B per lane and stored with fully coalesced 16-B global stores (a 1-KiB span per
 // instruction).  Storing straight from the MFMA layout touches 32 rows per instruction with 8-16 B
 // each, which made the epilogue dominate short kernels.
-template <int D, typename T>
+// NPASS > 1 stages D / NPASS columns at a time through a proportionally smaller region (kernels
+// whose LDS budget is set by the ring, not by the epilogue).
+template <int D, typename T, int NPASS = 1>
 struct RowTile {
-  static constexpr int PITCH = D * (int)sizeof(T) + 16;
+  static constexpr int DC = D / NPASS;                      // columns per pass
+  static constexpr int PITCH = DC * (int)sizeof(T) + 16;
   static constexpr int BYTES = 32 * PITCH;
 };
-template <int D, typename T>
+template <int D, typename T, int NPASS = 1>
 QA_DEVICE void store_rows(const v16f* acc, float sc, char* lds, T* dst_row0, int lane) {
-  using RT = RowTile<D, T>;
+  using RT = RowTile<D, T, NPASS>;
+  constexpr int NBP = D / 32 / NPASS;                        // 32-wide d blocks per pass
   const int h = lane >> 5, c32 = lane & 31;
 #pragma unroll
-  for (int b = 0; b < D / 32; ++b) {
+  for (int pass = 0; pass < NPASS; ++pass) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      char* p = lds + c32 * RT::PITCH + (32 * b + 8 * g + 4 * h) * (int)sizeof(T);
-      if constexpr (sizeof(T) == 2) {
-        v4h w;
+    for (int bb = 0; bb < NBP; ++bb) {
+      const int b = pass * NBP + bb;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * sc);
-        *reinterpret_cast<v4h*>(p) = w;
-      } else {
-        v4f w;
+      for (int g = 0; g < 4; ++g) {
+        char* p = lds + c32 * RT::PITCH + (32 * bb + 8 * g + 4 * h) * (int)sizeof(T);
+        if constexpr (sizeof(T) == 2) {
+          v4h w;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = acc[b][4 * g + j] * sc;
-        *reinterpret_cast<v4f*>(p) = w;
+          for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * sc);
+          *reinterpret_cast<v4h*>(p) = w;
+        } else {
+          v4f w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] = acc[b][4 * g + j] * sc;
+          *reinterpret_cast<v4f*>(p) = w;
+        }
       }
     }
-  }
-  constexpr int CPR = D * (int)sizeof(T) / 16;   // 16-B chunks per row
-  constexpr int RPI = 64 / CPR;                  // rows per instruction
-  const int r = lane / CPR, c = lane % CPR;
+    constexpr int CPR = RT::DC * (int)sizeof(T) / 16;   // 16-B chunks per staged row
+    constexpr int RPI = 64 / CPR;                       // rows per instruction
+    const int r = lane / CPR, c = lane % CPR;
 #pragma unroll
-  for (int i = 0; i < 32 / RPI; ++i) {
-    const int row = i * RPI + r;
-    const v4u v = *reinterpret_cast<const v4u*>(lds + row * RT::PITCH + 16 * c);
-    *reinterpret_cast<v4u*>(reinterpret_cast<char*>(dst_row0) + (long)row * D * (long)sizeof(T) + 16 * c) = v;
+    for (int i = 0; i < 32 / RPI; ++i) {
+      const int row = i * RPI + r;
+      const v4u v = *reinterpret_cast<const v4u*>(lds + row * RT::PITCH + 16 * c);
+      *reinterpret_cast<v4u*>(reinterpret_cast<char*>(dst_row0) + (long)row * D * (long)sizeof(T) +
+                              pass * RT::DC * (int)sizeof(T) + 16 * c) = v;
+    }
   }
 }
 

@@ -398,14 +398,24 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       v4i kf[C::NKS];
       qk_load(tn, kf);
       v8h va[2 * C::NDB];
+#if defined(QA_FWD_VLATE)
+      // the V reads join the LDS queue only after this wave's K reads have returned, so the K reads
+      // of the other waves of the workgroup (all released by the same barrier) are not queued
+      // behind 4 x 16 transposed V reads
+      const v16i nacc = qk_mma(kf);
+      __builtin_amdgcn_sched_barrier(0);
       pv_load(t, va);
+      __builtin_amdgcn_sched_barrier(0);
+#else
+      pv_load(t, va);
+#endif
 #if defined(QA_FWD_SB)
       __builtin_amdgcn_sched_barrier(0);   // LDS reads issue first; the softmax VALU covers their latency
       v4u pw[2];
       sm2(st, pw);
       __builtin_amdgcn_sched_barrier(0);
       const v16i nacc = qk_mma(kf);
-#else
+#elif !defined(QA_FWD_VLATE)
       const v16i nacc = qk_mma(kf);
 #endif
       QA_STAMP(2)
