@@ -58,6 +58,16 @@ int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, cons
                         const void* vdq, void* out, void* lse, long bh, long seq, int head_dim,
                         float qks, void* stream);
 
+/* Generalised shapes (the reference's int8 path has none of these): bh = batch *
+ * query heads with sq_tok query rows each; the key/value tensors have bh / group heads of sk_tok
+ * rows (query head h reads key/value head h / group: grouped-query attention); causal != 0 keeps
+ * key <= query (top-left aligned positions), masked scores are excluded.  Block scales index the
+ * query rows and the key/value rows separately.  sq_tok % 32 == sk_tok % 32 == 0, bh % group == 0.
+ * qattn_int8_attn_fwd is this with sq_tok = sk_tok = seq, group = 1, causal = 0. */
+int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
+                           const void* vdq, void* out, void* lse, long bh, long sq_tok, long sk_tok,
+                           int group, int causal, int head_dim, float qks, void* stream);
+
 /* Backward prologue, one pass (attention_int8.py:372-374, 398): dO f16 -> dO_i8 [rows, D] + sdO f16
  * [rows/32] (same quantiser), dO_bf = bf16(dO_i8) [rows, D] (optional, NULL to skip), and LD f32x2
  * [rows] = {f32(lse), f32(f16(rowsum(dO*O)))}. */
@@ -78,6 +88,15 @@ int qattn_int8_attn_bwd(const void* dO_i8, const void* sdO, const void* q_i8, co
                         const void* LD, const void* q_bf, const void* k_bf, const void* dO_bf,
                         void* dq, void* dk, void* dv, long bh, long seq, int head_dim, float qks,
                         float sms, void* stream);
+
+/* qattn_int8_attn_bwd for the generalised shapes of qattn_int8_attn_fwd_ex: dq, dO and the
+ * query-side tensors have bh heads of sq_tok rows, dk, dv and the key/value side bh / group heads of
+ * sk_tok rows (dk, dv of a key/value head sum over its group of query heads). */
+int qattn_int8_attn_bwd_ex(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                           const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                           const void* LD, const void* q_bf, const void* k_bf, const void* dO_bf,
+                           void* dq, void* dk, void* dv, long bh, long sq_tok, long sk_tok, int group,
+                           int causal, int head_dim, float qks, float sms, void* stream);
 
 /* The parts of qattn_int8_attn_bwd, launchable alone (per-kernel timing / overlap):
  * dK and dV (attention_int8.py:375-378, 423-428), dV only, dK only, dQ only (414-420). */

@@ -172,7 +172,7 @@ def quant_blocks(x, block=32):
     return idx.reshape(*lead, N, D), s
 
 
-def int8_fwd(q, k, v, block=32):
+def int8_fwd(q, k, v, block=32, causal=False):
     """Per-(batch, head) restatement of helion_atten_int8_hl_dot_fwd (int8:101-262).
 
     q, k, v fp16 [B,H,S,D], S % 32 == 0.  Returns the reference's 10-tuple
@@ -180,14 +180,21 @@ def int8_fwd(q, k, v, block=32):
     Bq, Bkv) with N = B*H*S and block index (b*H+h)*S/32 + s/32 (int8:161-168).  Attention is per
     (b, h) (build contract); quantisation is identical to the flattened reference
     whenever S % 32 == 0.
+
+    Extensions (no reference counterpart): k, v may have Hkv = H / G heads (query
+    head h reads key/value head h // G) and Sk != S tokens; ``causal`` drops key > query (top-left
+    aligned) by excluding those scores (P = 0; a tile with no kept key has sp = 0).
     """
     B, H, S, D = q.shape
-    Sk = k.shape[2]
+    Hkv, Sk = k.shape[1], k.shape[2]
+    G = H // Hkv
     BH = B * H
     qks = qk_scale(D)
     qi, sq = quant_blocks(q.reshape(BH, S, D), block)  # int8:178-186
-    ki, sk = quant_blocks(k.reshape(BH, Sk, D), block)  # int8:188-195
-    vi, sv = quant_blocks(v.reshape(BH, Sk, D), block)  # int8:241-247
+    ki_kv, sk_kv = quant_blocks(k.reshape(B * Hkv, Sk, D), block)  # int8:188-195
+    vi_kv, sv_kv = quant_blocks(v.reshape(B * Hkv, Sk, D), block)  # int8:241-247
+    kvh = torch.arange(BH) // G  # key/value head of each query head
+    ki, sk, vi, sv = ki_kv[kvh], sk_kv[kvh], vi_kv[kvh], sv_kv[kvh]
     nq = S // block
     O = torch.zeros((BH, S, D), dtype=torch.float32)  # int8:172
     l = torch.ones((BH, S, 1), dtype=torch.float32)  # int8:173
@@ -199,6 +206,9 @@ def int8_fwd(q, k, v, block=32):
         acc = _f(qd @ ki[:, k0:k1].double().transpose(1, 2))  # int8:197 (exact integer dot)
         Sf = ((acc * sqf) * _f(sk[:, t])[:, None, None]) * qks  # int8:200
         S16 = _h(Sf)  # int8:203
+        if causal:
+            keep = torch.arange(k0, k1)[None, :] <= torch.arange(S)[:, None]
+            S16 = torch.where(keep[None], S16, torch.full_like(S16, float("-inf")))
         rm = S16.amax(-1, keepdim=True)  # int8:205
         nm = torch.maximum(m, rm)  # int8:206-209
         P = torch.exp2(_f(_h(_f(S16) - _f(nm))))  # int8:211-213
@@ -208,14 +218,15 @@ def int8_fwd(q, k, v, block=32):
         l = l * r + lt  # int8:223
         O = O * r  # int8:225
         sp = torch.exp2(_f(_h(_f(rm) - _f(m)))) / 127  # int8:232-234
-        Pi = torch.trunc(P / sp)  # int8:236-237
+        Pi = torch.where(sp > 0, torch.trunc(P / torch.where(sp > 0, sp, 1.0)), 0.0)  # int8:236-237
         pv = _f(Pi.double() @ vi[:, k0:k1].double())  # int8:249
         O = O + (pv * sp) * _f(sv[:, t])[:, None, None]  # int8:249-250
     lse = _h(_f(m.squeeze(-1)) + _f(_h(torch.log2(l).squeeze(-1))))  # int8:252
     Oh = _h(O / l)  # int8:256-257
     N = BH * S
-    return (Oh.view(B, H, S, D), lse.reshape(N), qi.reshape(N, D), ki.reshape(BH * Sk, D).t(),
-            vi.reshape(BH * Sk, D), sq.reshape(-1), sk.reshape(-1), sv.reshape(-1), block, block)
+    Nkv = B * Hkv * Sk
+    return (Oh.view(B, H, S, D), lse.reshape(N), qi.reshape(N, D), ki_kv.reshape(Nkv, D).t(),
+            vi_kv.reshape(Nkv, D), sq.reshape(-1), sk_kv.reshape(-1), sv_kv.reshape(-1), block, block)
 
 
 def k_smooth(k):
@@ -227,46 +238,59 @@ def k_smooth(k):
     return _h(_f(k) - _f(km)), km
 
 
-def int8_bwd(dO, q_i8, sq, k_i8T, k_mean, sk, v_i8, sv, O, lse, Bq=32, Bkv=32):
+def int8_bwd(dO, q_i8, sq, k_i8T, k_mean, sk, v_i8, sv, O, lse, Bq=32, Bkv=32, causal=False,
+             kv_heads=None):
     """Corrected per-(b,h) restatement of helion_atten_int8_hl_dot_bwd (int8:268-432).
 
     Follows the reference's quantisation recipe (P and dS per Bq x Bkv tile, dO per Bq-row block,
     q/k/v int8 from the forward) with the build-contract fixes: dS = P*(dP-D)
     (int8:399), sm_scale (int8:417,424), per-(b,h) accumulation of dq/dk/dv in fp32 over all tiles
     (int8:420,427,428 overwrite / race), no k_mean term (int8:408-410; it multiplies rowsum(dS)=0).
-    Returns fp16 dq, dk, dv [B,H,S,D].
+    Returns fp16 dq, dk, dv [B,H,S,D].  Extensions as int8_fwd: key/value heads ``kv_heads`` (default
+    k_mean's, else H; dk, dv of a key/value head sum over its query heads in fp32), Sk != S from
+    k_i8T, ``causal`` (masked P = 0 before the tile quantisation).
     """
     B, H, S, D = O.shape
     BH = B * H
     N = BH * S
+    if kv_heads is None:
+        kv_heads = k_mean.shape[1] if k_mean is not None and k_mean.dim() == 4 else H
+    Hkv = kv_heads
+    G = H // Hkv
+    Sk = k_i8T.shape[1] // (B * Hkv)
+    kvh = torch.arange(BH) // G
     sms = sm_scale(D)
     qks = qk_scale(D)
     qi = q_i8.reshape(BH, S, D).double()
-    ki = k_i8T.t().reshape(BH, S, D).double()
-    vi = v_i8.reshape(BH, S, D).double()
+    ki = k_i8T.t().reshape(B * Hkv, Sk, D).double()[kvh]
+    vi = v_i8.reshape(B * Hkv, Sk, D).double()[kvh]
     sq = _f(sq.reshape(BH, S // Bq))
-    sk = _f(sk.reshape(BH, S // Bkv))
-    sv = _f(sv.reshape(BH, S // Bkv))
+    sk = _f(sk.reshape(B * Hkv, Sk // Bkv))[kvh]
+    sv = _f(sv.reshape(B * Hkv, Sk // Bkv))[kvh]
     dOh = dO.reshape(BH, S, D)
     Oh = O.reshape(BH, S, D)
     lse = lse.reshape(BH, S)
     dq = torch.zeros((BH, S, D))
-    dk = torch.zeros((BH, S, D))
-    dv = torch.zeros((BH, S, D))
+    dk = torch.zeros((BH, Sk, D))
+    dv = torch.zeros((BH, Sk, D))
     dOi, sdO = quant_blocks(dOh, Bq)  # int8:372-374
     dOi = dOi.double()
     sdO = _f(sdO)
     # D = rowsum(dO*O) in fp16 (int8:398): elementwise fp16 product, fp32-accumulated sum -> fp16
     Dr = _f(_h(_f(_h(_f(dOh) * _f(Oh))).sum(-1)))
-    for kt in range(S // Bkv):
+    for kt in range(Sk // Bkv):
         ks = slice(kt * Bkv, (kt + 1) * Bkv)
         for qt in range(S // Bq):
             qs = slice(qt * Bq, (qt + 1) * Bq)
             acc = _f(qi[:, qs] @ ki[:, ks].transpose(1, 2))  # int8:352
             S16 = _h(((acc * sq[:, qt, None, None]) * sk[:, kt, None, None]) * qks)  # int8:353-355
             P = torch.exp2(_f(_h(_f(S16) - _f(lse[:, qs])[..., None])))  # int8:360
+            if causal:
+                keep = torch.arange(ks.start, ks.stop)[None, :] <= torch.arange(qs.start, qs.stop)[:, None]
+                P = torch.where(keep[None], P, torch.zeros_like(P))
             sP = P.abs().flatten(1).amax(-1) / 127  # int8:363
-            Pi = torch.trunc(P / sP[:, None, None]).double()  # int8:364-365
+            sP_safe = torch.where(sP == 0, torch.ones_like(sP), sP)
+            Pi = torch.trunc(P / sP_safe[:, None, None]).double()  # int8:364-365
             dvt = ((_f(Pi.transpose(1, 2) @ dOi[:, qs]) * sdO[:, qt, None, None])
                    * sP[:, None, None])  # int8:375-377
             dv[:, ks] += dvt
@@ -281,7 +305,9 @@ def int8_bwd(dO, q_i8, sq, k_i8T, k_mean, sk, v_i8, sv, O, lse, Bq=32, Bkv=32):
             dkt = ((_f(dSi.transpose(1, 2) @ qi[:, qs]) * sdS[:, None, None])
                    * sq[:, qt, None, None]) * sms
             dk[:, ks] += dkt  # int8:423-427
-    return _h(dq).view(B, H, S, D), _h(dk).view(B, H, S, D), _h(dv).view(B, H, S, D)
+    dk = dk.view(B * Hkv, G, Sk, D).sum(1)
+    dv = dv.view(B * Hkv, G, Sk, D).sum(1)
+    return _h(dq).view(B, H, S, D), _h(dk).view(B, Hkv, Sk, D), _h(dv).view(B, Hkv, Sk, D)
 
 
 # --------------------------------------------------------------------------------------------

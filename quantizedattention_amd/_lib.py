@@ -26,6 +26,9 @@ SIGNATURES = {
     "qattn_int8_quant_img": [_vp] * 6 + [_c_long, _c_int, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_int8_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _c_float, _vp],
+    "qattn_int8_attn_fwd_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
+    "qattn_int8_attn_bwd_ex": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
+                                             _c_float, _vp],
     "qattn_int8_bwd_prep": [_vp] * 7 + [_c_long, _c_long, _c_int, _vp],
     "qattn_i8_to_bf16": [_vp, _vp, _c_long, _vp],
     "qattn_int8_attn_bwd": [_vp] * 15 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],

@@ -10,6 +10,12 @@ Public names (same signatures, argument meaning, outputs and assertion messages)
 Semantics follow the build contract of SURVEY.md §8a (rows A4-A6): attention per (batch, head)
 (F2), corrected backward (F4), SageAttention k-smoothing with the token mean (F1).  The
 ``helion_*`` names are kept for drop-in compatibility; no Helion/Triton is involved.
+
+Generalised shapes (extensions the reference does not have): q [B, Hq, Sq, D] with
+k, v [B, Hkv, Sk, D], Hq a multiple of Hkv (grouped-query attention: query head h reads key/value
+head h // (Hq/Hkv)), Sq != Sk, and ``causal=True`` (keep key <= query, top-left aligned positions;
+masked scores are excluded).  With Hq == Hkv, Sq == Sk and causal=False every function is exactly
+the reference-shaped one.
 """
 from __future__ import annotations
 
@@ -41,16 +47,17 @@ def _check_shapes(q, k, v):
     _, _, v_tokens, v_head_dim = v.shape
     assert k_tokens == v_tokens, "k and v tokens are different"
     assert k_head_dim == v_head_dim, "k head_dim and v head_dim are different"
-    if q_tokens != k_tokens or q_head_dim != k_head_dim or q.shape[:2] != k.shape[:2] \
-            or k.shape[:2] != v.shape[:2]:
-        raise _lib.QAttnError("qattn int8: q/k/v must share (batch, head, tokens, head_dim)")
-    if q_tokens % BQ != 0:
-        raise _lib.QAttnError(f"qattn int8: tokens must be a multiple of {BQ}")
+    if q_head_dim != k_head_dim or q.shape[0] != k.shape[0] or k.shape[:2] != v.shape[:2]:
+        raise _lib.QAttnError("qattn int8: q/k/v must share batch and head_dim, k/v their heads")
+    if head % k.shape[1] != 0:
+        raise _lib.QAttnError("qattn int8: query heads must be a multiple of key/value heads")
+    if q_tokens % BQ != 0 or k_tokens % BKV != 0:
+        raise _lib.QAttnError(f"qattn int8: token counts must each be a multiple of {BQ}")
     if q_head_dim not in (64, 128):
         raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
 
 
-def _int8_forward(q, k, v, smooth: bool, images: bool = False):
+def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = False):
     """Quantise q, k, v and run the int8 attention forward.
 
     Returns (O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean, q_bf, k_bf); q_bf / k_bf are the exact
@@ -63,46 +70,56 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False):
     k = k.to(torch.float16).contiguous()
     v = v.to(torch.float16).contiguous()
     B, H, S, D = q.shape
+    Hkv, Sk = k.shape[1], k.shape[2]
     N = B * H * S
+    Nkv = B * Hkv * Sk
     dev = q.device
     st = _lib.stream_of(q)
     q_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
-    k_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
-    v_i8 = torch.empty((N, D), dtype=torch.int8, device=dev)
+    k_i8 = torch.empty((Nkv, D), dtype=torch.int8, device=dev)
+    v_i8 = torch.empty((Nkv, D), dtype=torch.int8, device=dev)
     sq = torch.empty((N // BQ,), dtype=torch.float16, device=dev)
-    sk = torch.empty((N // BKV,), dtype=torch.float16, device=dev)
-    sv = torch.empty((N // BKV,), dtype=torch.float16, device=dev)
-    vdq = torch.empty((N, D), dtype=torch.float16, device=dev)  # workspace fp16(v_i8 * sv)
+    sk = torch.empty((Nkv // BKV,), dtype=torch.float16, device=dev)
+    sv = torch.empty((Nkv // BKV,), dtype=torch.float16, device=dev)
+    vdq = torch.empty((Nkv, D), dtype=torch.float16, device=dev)  # workspace fp16(v_i8 * sv)
     O = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
     lse = torch.empty((N,), dtype=torch.float16, device=dev)
     q_bf = k_bf = None
     if images:
         q_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
-        k_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
+        k_bf = torch.empty((Nkv, D), dtype=torch.bfloat16, device=dev)
     k_mean = None
     if smooth:
-        k_mean = torch.empty((B, H, 1, D), dtype=torch.float16, device=dev)
-        _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(k_mean), B * H, S, D, st)
+        k_mean = torch.empty((B, Hkv, 1, D), dtype=torch.float16, device=dev)
+        _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(k_mean), B * Hkv, Sk, D, st)
     _lib.call("qattn_int8_quant_img", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), None, _lib.ptr(q_bf),
               None, N, S, D, st)
     _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
-              _lib.ptr(k_mean), N, S, D, st)
+              _lib.ptr(k_mean), Nkv, Sk, D, st)
     _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vdq), None,
-              N, S, D, st)
-    _lib.call("qattn_int8_attn_fwd", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
-              _lib.ptr(vdq), _lib.ptr(O), _lib.ptr(lse), B * H, S, D,
+              Nkv, Sk, D, st)
+    _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
+              _lib.ptr(vdq), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, int(bool(causal)), D,
               float(torch.tensor(_qk_scale(D), dtype=torch.float32)), st)
     # k_i8T is returned as the [D, N] view of the row-major [N, D] tensor (same values/shape as
     # int8:165, zero-copy).
     return O, lse, q_i8, k_i8.t(), v_i8, sq, sk, sv, k_mean, q_bf, k_bf
 
 
-def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=None):
-    """Corrected int8 backward; q_bf / k_bf: bf16 images from the forward (computed here if None)."""
+def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=None, causal=False,
+                   kv_heads=None):
+    """Corrected int8 backward; q_bf / k_bf: bf16 images from the forward (computed here if None).
+
+    kv_heads: key/value heads (default: those of O); their token count follows from k_i8T."""
     O = O.to(torch.float16).contiguous()
     dO = dO.to(torch.float16).contiguous()
     _lib.require_gpu(dO, O, q_i8)
     B, H, S, D = O.shape
+    Hkv = H if kv_heads is None else int(kv_heads)
+    Nkv = k_i8T.shape[1]
+    if H % Hkv != 0 or Nkv % (B * Hkv) != 0:
+        raise _lib.QAttnError("qattn int8 backward: inconsistent key/value heads")
+    Sk = Nkv // (B * Hkv)
     N = B * H * S
     dev = O.device
     st = _lib.stream_of(O)
@@ -121,18 +138,18 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
         q_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
         _lib.call("qattn_i8_to_bf16", _lib.ptr(q_i8), _lib.ptr(q_bf), N * D, st)
     if k_bf is None:
-        k_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
-        _lib.call("qattn_i8_to_bf16", _lib.ptr(k_i8), _lib.ptr(k_bf), N * D, st)
+        k_bf = torch.empty((Nkv, D), dtype=torch.bfloat16, device=dev)
+        _lib.call("qattn_i8_to_bf16", _lib.ptr(k_i8), _lib.ptr(k_bf), Nkv * D, st)
     dq = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
-    dk = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
-    dv = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
+    dk = torch.empty((B, Hkv, Sk, D), dtype=torch.float16, device=dev)
+    dv = torch.empty((B, Hkv, Sk, D), dtype=torch.float16, device=dev)
     qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
     sms = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
-    _lib.call("qattn_int8_attn_bwd", _lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8),
+    _lib.call("qattn_int8_attn_bwd_ex", _lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8),
               _lib.ptr(sq.contiguous()), _lib.ptr(k_i8), _lib.ptr(sk.contiguous()),
               _lib.ptr(v_i8), _lib.ptr(sv.contiguous()), _lib.ptr(LD), _lib.ptr(q_bf),
               _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
-              B * H, S, D, qks, sms, st)
+              B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms, st)
     return dq, dk, dv
 
 
@@ -140,11 +157,13 @@ def helion_atten_int8_hl_dot_fwd(
     q_fp16_input: torch.Tensor,
     k_fp16_input: torch.Tensor,
     v_fp16_input: torch.Tensor,
+    causal: bool = False,
 ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
            torch.Tensor, torch.Tensor, torch.Tensor, int, int]:
-    """int8 forward (int8:101-262): returns (O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv)."""
+    """int8 forward (int8:101-262): returns (O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv).
+    ``causal`` (and GQA / Sq != Sk shapes) are extensions, see the module docstring."""
     O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, _, _, _ = _int8_forward(
-        q_fp16_input, k_fp16_input, v_fp16_input, smooth=False)
+        q_fp16_input, k_fp16_input, v_fp16_input, smooth=False, causal=causal)
     return O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, BQ, BKV
 
 
@@ -161,16 +180,22 @@ def helion_atten_int8_hl_dot_bwd(
     lse_input_fp16: torch.Tensor,
     Bq: int,
     Bkv: int,
+    causal: bool = False,
+    kv_heads: int | None = None,
 ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Corrected int8 backward (int8:268-432): returns fp16 (dq, dk, dv) [B,H,S,D].
 
     k_mean is accepted for signature compatibility; its term multiplies rowsum(dS) = 0 and is
-    dropped (build contract).
+    dropped (build contract).  Its head count (``[B, Hkv, 1, D]``) gives the key/value heads of a
+    grouped-query call unless ``kv_heads`` is passed.
     """
     if Bq != BQ or Bkv != BKV:
         raise _lib.QAttnError("qattn int8 backward is built for Bq = Bkv = 32")
+    if kv_heads is None and k_mean_bh_fp16 is not None and k_mean_bh_fp16.dim() == 4:
+        kv_heads = k_mean_bh_fp16.shape[1]
     return _int8_backward(dO_input_fp16, q_bh_int8, sq_bh_fp16, k_bh_int8_T, sk_bh_fp16, v_bh_int8,
-                          sv_bh_fp16, O_input_fp16, lse_input_fp16)
+                          sv_bh_fp16, O_input_fp16, lse_input_fp16, causal=causal,
+                          kv_heads=kv_heads)
 
 
 class SageAttention3_Int8_autograd_function(Function):
@@ -178,12 +203,15 @@ class SageAttention3_Int8_autograd_function(Function):
     (O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv)."""
 
     @staticmethod
-    def forward(ctx, q_fp16, k_fp16, v_fp16):
+    def forward(ctx, q_fp16, k_fp16, v_fp16, *opts):
+        # opts: (causal,) -- an extension; the reference's apply(q, k, v) passes none
+        causal = bool(opts[0]) if opts else False
         # The bf16 images of q_i8 / k_i8 the backward reads come out of the same quantiser pass
         # when a gradient will be taken (kept on ctx, not returned: the 11-tuple is the reference's).
         images = any(t.requires_grad for t in (q_fp16, k_fp16, v_fp16))
         O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean, q_bf, k_bf = _int8_forward(
-            q_fp16, k_fp16, v_fp16, smooth=True, images=images)
+            q_fp16, k_fp16, v_fp16, smooth=True, images=images, causal=causal)
+        ctx.opts = (causal, k_fp16.shape[1], len(opts))
         ctx.mark_non_differentiable(lse, k_mean, sq, sk, sv)  # int8:52-56
         ctx.save_for_backward(O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv)  # int8:58-64
         ctx.images = (q_bf, k_bf)
@@ -200,10 +228,15 @@ class SageAttention3_Int8_autograd_function(Function):
             dO_fp16 = torch.zeros_like(O)
         q_bf, k_bf = ctx.images
         ctx.images = None
-        dq, dk, dv = _int8_backward(dO_fp16, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf, k_bf)
-        return dq, dk, dv
+        causal, kv_heads, nopts = ctx.opts
+        dq, dk, dv = _int8_backward(dO_fp16, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf, k_bf,
+                                    causal=causal, kv_heads=kv_heads)
+        return (dq, dk, dv) + (None,) * nopts
 
 
-def sage_attention_3_int8(q_fp16, k_fp16, v_fp16):
-    """int8:434-451: SageAttention3 int8 attention with autograd; returns O fp16."""
+def sage_attention_3_int8(q_fp16, k_fp16, v_fp16, causal: bool = False):
+    """int8:434-451: SageAttention3 int8 attention with autograd; returns O fp16.
+    ``causal`` (and GQA / Sq != Sk shapes) are extensions, see the module docstring."""
+    if causal:
+        return SageAttention3_Int8_autograd_function.apply(q_fp16, k_fp16, v_fp16, True)[0]
     return SageAttention3_Int8_autograd_function.apply(q_fp16, k_fp16, v_fp16)[0]

@@ -31,6 +31,8 @@
 // Deferred max (cdna_hip_programming.md T13): the running max m moves only when some row's tile max
 // exceeds it by more than THR = 8 (log2 units); P_i8 depends only on S - rowmax(tile), O and l share
 // the (possibly stale) reference, so O / l is unchanged up to rounding and operands stay <= 2^8.
+#include <climits>
+
 #include "common.h"
 
 namespace qattn {
@@ -133,18 +135,22 @@ struct SmTile {
 // 2 = no PV MFMA, 3 = no QK^T MFMA, 4 = no K/V streaming (ring slot 0 reused, no barriers),
 // 5 = 4 + no softmax, 6 = 1 + half the V-operand LDS reads, 7 = 1 + half the K-operand LDS reads.
 // Outputs of AB != 0 are meaningless.
-template <int D, int AB = 0>
+// Shapes: BH = batch * query heads, Sq query and Sk key tokens per head; query head
+// bh reads key/value head bh / G (grouped-query attention, G = Hq / Hkv).  CAUSAL keeps key <= query
+// (top-left aligned indices); masked scores are excluded (P = 0).  The reference has neither (its
+// int8 path is square, ungrouped and non-causal, int8:122-127, 344); these are extensions.
+template <int D, int AB = 0, bool CAUSAL = false>
 __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
     const _Float16* __restrict__ sk, const _Float16* __restrict__ vdq, _Float16* __restrict__ out,
-    _Float16* __restrict__ lse, int BH, int S, float qks) {
+    _Float16* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks) {
   using C = Int8FwdCfg<D>;
   constexpr bool STREAM = AB != 4 && AB != 5;
   constexpr bool SOFTMAX = AB != 1 && AB != 5 && AB != 6 && AB != 7;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   _Float16* sk_lds = reinterpret_cast<_Float16*>(smem + C::NSLOT * C::SLOT);
 
-  const int nq = (S + C::QROWS - 1) / C::QROWS;
+  const int nq = (Sq + C::QROWS - 1) / C::QROWS;
   int bh, qt;
   xcd_remap(blockIdx.x, nq, BH, bh, qt);
   const int tid = threadIdx.x;
@@ -153,21 +159,23 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
   const int h = lane >> 5;
   const int c32 = lane & 31;
   const int q0 = qt * C::QROWS + wave * 32;
-  const bool active = q0 < S;
-  const long head_row0 = (long)bh * S;
-  const int8_t* kbase = k_i8 + head_row0 * D;
-  const _Float16* vbase = vdq + head_row0 * D;
-  const int nt = S / C::KT;
+  const bool active = q0 < Sq;
+  const long head_row0 = (long)bh * Sq;           // this head's query rows
+  const long kv_row0 = (long)(bh / G) * Sk;       // its key/value head's rows
+  const int8_t* kbase = k_i8 + kv_row0 * D;
+  const _Float16* vbase = vdq + kv_row0 * D;
+  // causal: key tiles past the workgroup's last query are masked for all of its rows
+  const int nt = CAUSAL ? min(Sk / C::KT, (qt * C::QROWS + C::QROWS) / C::KT) : Sk / C::KT;
 
   DmaPlan<D> dma;
-  dma.init(wave, lane, S, kbase, vbase);
+  dma.init(wave, lane, Sk, kbase, vbase);
   const unsigned smem_lds = lds_addr(smem);
   dma.issue(smem_lds, 0);
   if (STREAM) {
     dma.issue(smem_lds + 1 * C::SLOT, min(1, nt - 1));
     dma.issue(smem_lds + 2 * C::SLOT, min(2, nt - 1));
   }
-  for (int i = tid; i < nt; i += 64 * C::WAVES) sk_lds[i] = sk[head_row0 / 32 + i];
+  for (int i = tid; i < nt; i += 64 * C::WAVES) sk_lds[i] = sk[kv_row0 / 32 + i];
 
   // ---- Q fragment (B operand of S^T = K Q^T): lane holds Q[q0+c32][32s + 16h .. +16]
   v4i qf[C::NKS];
@@ -236,7 +244,16 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
   //   (a) row max of the int32 scores and d = f16(S - rm): independent of the running max, so it
   //       shares a basic block with the PV MFMAs of the previous tile;
   //   (b) deferred running-max update (rare branch), er = exp2(rm - m), sp = f16(er / 127).
-  auto sm1a = [&](const v16i& acc, float c, SmTile& st) -> _Float16 {
+  auto sm1a = [&](const v16i& acc_in, float c, SmTile& st, int t) -> _Float16 {
+    // causal tiles crossing this wave's diagonal: keys above the row's query drop out of the max
+    // (INT_MIN) and get d = -inf below, so P = 0 and the tile scale sp ignores them
+    const bool diag = CAUSAL && (t * C::KT + C::KT - 1 > q0);
+    v16i acc = acc_in;
+    if (diag) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (t * C::KT + (r & 3) + 8 * (r >> 2) + 4 * h > q0 + c32) acc[r] = INT_MIN;
+    }
     int mx = imax3(acc[0], acc[1], acc[2]);
     mx = imax3(mx, acc[3], acc[4]);
     mx = imax3(mx, acc[5], acc[6]);
@@ -259,6 +276,14 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
     const v2h rm2 = {rm, rm};
 #pragma unroll
     for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;   // f16(S - rm)  (int8:211, 232-236)
+    if (diag) {
+      const _Float16 ninf = (_Float16)(-INFINITY);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          if (acc[2 * j + e] == INT_MIN) st.d[j][e] = ninf;
+    }
     return rm;
   };
   auto sm1b = [&](_Float16 rm, SmTile& st) {
@@ -361,7 +386,7 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
   SmTile st;
   if (active) {
     const v16i acc0 = qk(0);
-    if constexpr (SOFTMAX) sm1b(sm1a(acc0, cq * (float)sk_lds[0], st), st);
+    if constexpr (SOFTMAX) sm1b(sm1a(acc0, cq * (float)sk_lds[0], st, 0), st);
     else st.d[0] = __builtin_bit_cast(v2h, acc0[0]);
   }
   // Steady state: one basic block per tile (except the rare running-max rescale).  The last
@@ -434,7 +459,7 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       pv_mma(va, pw);
       QA_STAMP(4)
       if constexpr (SOFTMAX) {
-        const _Float16 rm = sm1a(nacc, cn, st);
+        const _Float16 rm = sm1a(nacc, cn, st, tn);
         QA_STAMP(5)
         sm1b(rm, st);
       } else {
@@ -466,19 +491,19 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
                           out + (head_row0 + q0) * D, lane);
 }
 
-template <int D, int AB>
+template <int D, int AB, bool CAUSAL>
 static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                      const void* vdq, void* out, void* lse, long bh, long seq, float qks,
-                      hipStream_t st) {
+                      const void* vdq, void* out, void* lse, long bh, long sq_tok, long sk_tok, int group,
+                      float qks, hipStream_t st) {
   using C = Int8FwdCfg<D>;
-  const int nq = (int)((seq + C::QROWS - 1) / C::QROWS);
-  const int lds = C::NSLOT * C::SLOT + (int)(((seq / 32) * 2 + 15) / 16 * 16);
-  hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<D, AB>,
+  const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
+  const int lds = C::NSLOT * C::SLOT + (int)(((sk_tok / 32) * 2 + 15) / 16 * 16);
+  hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<D, AB, CAUSAL>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((int8_attn_fwd_kernel<D, AB>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES),
-                     lds, st, (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8,
-                     (const _Float16*)sk, (const _Float16*)vdq, (_Float16*)out, (_Float16*)lse,
-                     (int)bh, (int)seq, qks);
+  hipLaunchKernelGGL((int8_attn_fwd_kernel<D, AB, CAUSAL>), dim3((unsigned)(nq * bh)),
+                     dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
+                     (const int8_t*)k_i8, (const _Float16*)sk, (const _Float16*)vdq, (_Float16*)out,
+                     (_Float16*)lse, (int)bh, (int)sq_tok, (int)sk_tok, group, qks);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -486,14 +511,27 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
 
 using namespace qattn;
 
+extern "C" int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const void* k_i8,
+                                      const void* sk, const void* vdq, void* out, void* lse, long bh,
+                                      long sq_tok, long sk_tok, int group, int causal, int head_dim,
+                                      float qks, void* stream) {
+  if (sq_tok % 32 != 0 || sk_tok % 32 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128))
+    return 1;
+  if (bh == 0 || sq_tok == 0) return 0;
+  if (sk_tok == 0) return 1;
+  hipStream_t st = (hipStream_t)stream;
+#define QA_L(Dv, CV) launch_fwd<Dv, 0, CV>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, sq_tok, sk_tok, group, qks, st)
+  if (head_dim == 128) return causal ? QA_L(128, true) : QA_L(128, false);
+  return causal ? QA_L(64, true) : QA_L(64, false);
+#undef QA_L
+}
+
 extern "C" int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
                                    const void* vdq, void* out, void* lse, long bh, long seq,
                                    int head_dim, float qks, void* stream) {
-  if (seq % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  if (bh == 0 || seq == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  if (head_dim == 128) return launch_fwd<128, 0>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
-  return launch_fwd<64, 0>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
+  return qattn_int8_attn_fwd_ex(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, 0, head_dim, qks,
+                                stream);
 }
 
 extern "C" int qattn_int8_attn_fwd_ablate(const void* q_i8, const void* sq, const void* k_i8,
@@ -502,14 +540,14 @@ extern "C" int qattn_int8_attn_fwd_ablate(const void* q_i8, const void* sq, cons
   if (seq % 32 != 0 || bh == 0) return 1;
   hipStream_t st = (hipStream_t)stream;
   switch (ab) {
-    case 1: return launch_fwd<128, 1>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
-    case 2: return launch_fwd<128, 2>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
-    case 3: return launch_fwd<128, 3>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
-    case 4: return launch_fwd<128, 4>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
-    case 5: return launch_fwd<128, 5>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
-    case 6: return launch_fwd<128, 6>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
-    case 7: return launch_fwd<128, 7>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
-    default: return launch_fwd<128, 0>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, qks, st);
+    case 1: return launch_fwd<128, 1, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
+    case 2: return launch_fwd<128, 2, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
+    case 3: return launch_fwd<128, 3, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
+    case 4: return launch_fwd<128, 4, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
+    case 5: return launch_fwd<128, 5, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
+    case 6: return launch_fwd<128, 6, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
+    case 7: return launch_fwd<128, 7, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
+    default: return launch_fwd<128, 0, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
   }
 }
 

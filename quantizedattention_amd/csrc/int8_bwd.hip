@@ -252,7 +252,11 @@ QA_DEVICE float max16_abs3(const float* x) {
   return fmaxf(m, fabsf(x[15]));
 }
 
-template <int D, int ROLE>
+// Shapes: the own side has BHx heads of Sx rows; own head bh streams the Ny rows
+// starting at row (bh / ydiv) * Ny of the streamed tensors -- dK/dV: the G query heads that share a
+// key/value head (Ny = G * Sq, contiguous), dQ: the key/value head of the query head (ydiv = G,
+// Ny = Sk).  CAUSAL drops key > query (positions: streamed row mod Smod).
+template <int D, int ROLE, bool CAUSAL = false>
 __global__ __launch_bounds__((64 * BwdCfg<D, ROLE>::WAVES), (8 / BwdCfg<D, ROLE>::WAVES))
 void int8_bwd_kernel(
     const int8_t* __restrict__ x8a, const int8_t* __restrict__ x8b, const _Float16* __restrict__ sxa,
@@ -260,26 +264,28 @@ void int8_bwd_kernel(
     const __bf16* __restrict__ ytr, const __bf16* __restrict__ ytr2, const float2* __restrict__ yld,
     const _Float16* __restrict__ sya, const _Float16* __restrict__ syb,
     const float2* __restrict__ xld, _Float16* __restrict__ out, _Float16* __restrict__ out2, int BH,
-    int S, float qks, float sms) {
+    int Sx, int Ny, int ydiv, int Smod, float qks, float sms) {
   using C = I8BwdCfg<D>;
   using G = BwdCfg<D, ROLE>;
   constexpr bool TWO = G::TWO;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nxb = (S + G::XROWS - 1) / G::XROWS;
+  const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
   int bh, xt;
   xcd_remap(blockIdx.x, nxb, BH, bh, xt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
   const int x0 = xt * G::XROWS + wave * 32;
-  const bool active = x0 < S;
-  const long hrow = (long)bh * S;
-  const int nt = S / 32;
+  const bool active = x0 < Sx;
+  const long hrow = (long)bh * Sx;                 // own rows
+  const long yrow = (long)(bh / ydiv) * Ny;        // streamed rows
+  // causal dQ: key tiles past the workgroup's last query are masked for all of its rows
+  const int nt = (CAUSAL && ROLE == ROLE_DQ) ? min(Ny / 32, (xt * G::XROWS + G::XROWS) / 32) : Ny / 32;
 
   BwdDma<D, ROLE> dma;
-  dma.init(wave, lane, S, reinterpret_cast<const char*>(y8a + hrow * D),
-           reinterpret_cast<const char*>(y8b + hrow * D), reinterpret_cast<const char*>(ytr + hrow * D),
-           reinterpret_cast<const char*>(ytr2 + hrow * D), reinterpret_cast<const char*>(yld + hrow));
+  dma.init(wave, lane, Ny, reinterpret_cast<const char*>(y8a + yrow * D),
+           reinterpret_cast<const char*>(y8b + yrow * D), reinterpret_cast<const char*>(ytr + yrow * D),
+           reinterpret_cast<const char*>(ytr2 + yrow * D), reinterpret_cast<const char*>(yld + yrow));
   const unsigned smem_lds = lds_addr(smem);
 #pragma unroll
   for (int i = 0; i < G::NSLOT - 1; ++i) dma.issue(smem_lds + i * G::SLOT, min(i, nt - 1), lane);
@@ -287,8 +293,8 @@ void int8_bwd_kernel(
   // hipcc wait vmcnt for the in-flight LDS-DMA)
   _Float16* sc_lds = reinterpret_cast<_Float16*>(smem + G::NSLOT * G::SLOT);
   for (int i = tid; i < nt; i += 64 * G::WAVES) {
-    sc_lds[i] = sya[hrow / 32 + i];
-    sc_lds[nt + i] = syb[hrow / 32 + i];
+    sc_lds[i] = sya[yrow / 32 + i];
+    sc_lds[nt + i] = syb[yrow / 32 + i];
   }
 
   // own-side int8 fragments (B operands): lane holds X[x0 + c32][32s + 16h .. +16]
@@ -347,6 +353,10 @@ void int8_bwd_kernel(
   };
   // fp32 P and/or dS of tile t
   auto values = [&](int t, const v16i& sa, const v16i& pa, float* P, float* dS) {
+    // causal: position of the tile's first streamed row; the mask is applied only on tiles that
+    // cross this wave's diagonal (the streamed side is queries for dK/dV, keys for dQ)
+    const int y0 = (32 * t) % Smod;
+    const bool diag = CAUSAL && (ROLE == ROLE_DQ ? (y0 + 31 > x0) : (x0 + 31 > y0));
     // c1 = sq*(sk*qks), c2 = sdO*sv with the streamed / own roles of each kernel
     const float sy_a = (float)sc_lds[t], sy_b = (float)sc_lds[nt + t];
     float c1, c2;
@@ -368,7 +378,8 @@ void int8_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
-          const float p = exp2_f32(fmaf((float)sa[i], c1, -lse_r[j]));
+          float p = exp2_f32(fmaf((float)sa[i], c1, -lse_r[j]));
+          if (diag && x0 + c32 > y0 + 8 * g + 4 * h + j) p = 0.f;   // key > query
           if constexpr (G::WANT_P) P[i] = p;
           if constexpr (G::WANT_DS) dS[i] = p * fmaf((float)pa[i], c2, -d_r[j]);
         }
@@ -380,7 +391,8 @@ void int8_bwd_kernel(
       const float k1 = -fmaf(c1, M, lsex), k2 = -fmaf(c2, M, Dx);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2_f32(fmaf(__int_as_float(sa[i]), c1, k1));
+        float p = exp2_f32(fmaf(__int_as_float(sa[i]), c1, k1));
+        if (diag && y0 + (i & 3) + 8 * (i >> 2) + 4 * h > x0 + c32) p = 0.f;   // key > query
         dS[i] = p * fmaf(__int_as_float(pa[i]), c2, k2);
       }
     }
@@ -548,64 +560,93 @@ extern "C" int qattn_i8_to_bf16(const void* x, void* y, long n, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+template <int D, int ROLE, bool CAUSAL>
+static void launch_bwd_c(const void* x8a, const void* x8b, const void* sxa, const void* sxb,
+                         const void* y8a, const void* y8b, const void* ytr, const void* ytr2,
+                         const void* yld, const void* sya, const void* syb, const void* xld, void* out,
+                         void* out2, long bhx, long sx, long ny, int ydiv, long smod, float qks,
+                         float sms, hipStream_t st) {
+  using G = BwdCfg<D, ROLE>;
+  const int lds = G::NSLOT * G::SLOT + (int)((2 * (ny / 32) * 2 + 15) / 16 * 16);
+  hipFuncSetAttribute((const void*)int8_bwd_kernel<D, ROLE, CAUSAL>,
+                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
+  hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE, CAUSAL>), dim3((unsigned)(nb * bhx)),
+                     dim3(64 * G::WAVES), lds, st, (const int8_t*)x8a, (const int8_t*)x8b,
+                     (const _Float16*)sxa, (const _Float16*)sxb, (const int8_t*)y8a,
+                     (const int8_t*)y8b, (const __bf16*)ytr, (const __bf16*)ytr2, (const float2*)yld,
+                     (const _Float16*)sya, (const _Float16*)syb, (const float2*)xld, (_Float16*)out,
+                     (_Float16*)out2, (int)bhx, (int)sx, (int)ny, ydiv, (int)smod, qks, sms);
+}
 template <int D, int ROLE>
-static void launch_bwd(const void* x8a, const void* x8b, const void* sxa, const void* sxb,
+static void launch_bwd(int causal, const void* x8a, const void* x8b, const void* sxa, const void* sxb,
                        const void* y8a, const void* y8b, const void* ytr, const void* ytr2,
                        const void* yld, const void* sya, const void* syb, const void* xld, void* out,
-                       void* out2, long bh, long seq, float qks, float sms, hipStream_t st) {
-  using G = BwdCfg<D, ROLE>;
-  const int lds = G::NSLOT * G::SLOT + (int)((2 * (seq / 32) * 2 + 15) / 16 * 16);
-  hipFuncSetAttribute((const void*)int8_bwd_kernel<D, ROLE>,
-                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  const int nb = (int)((seq + G::XROWS - 1) / G::XROWS);
-  hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES), lds,
-                     st, (const int8_t*)x8a, (const int8_t*)x8b, (const _Float16*)sxa,
-                     (const _Float16*)sxb, (const int8_t*)y8a, (const int8_t*)y8b,
-                     (const __bf16*)ytr, (const __bf16*)ytr2, (const float2*)yld,
-                     (const _Float16*)sya, (const _Float16*)syb, (const float2*)xld,
-                     (_Float16*)out, (_Float16*)out2, (int)bh, (int)seq, qks, sms);
+                       void* out2, long bhx, long sx, long ny, int ydiv, long smod, float qks,
+                       float sms, hipStream_t st) {
+  if (causal)
+    launch_bwd_c<D, ROLE, true>(x8a, x8b, sxa, sxb, y8a, y8b, ytr, ytr2, yld, sya, syb, xld, out, out2,
+                                bhx, sx, ny, ydiv, smod, qks, sms, st);
+  else
+    launch_bwd_c<D, ROLE, false>(x8a, x8b, sxa, sxb, y8a, y8b, ytr, ytr2, yld, sya, syb, xld, out, out2,
+                                 bhx, sx, ny, ydiv, smod, qks, sms, st);
 }
 
-// which: bit mask 1 = dV kernel, 4 = dK kernel, 8 = fused dK+dV kernel, 2 = dQ kernel
+// which: bit mask 1 = dV kernel, 4 = dK kernel, 8 = fused dK+dV kernel, 2 = dQ kernel.
+// bh = batch * query heads; the key/value side has bh / group heads of skt rows.
 template <int D>
 static void bwd_launch_d(int which, const void* dO_i8, const void* sdO, const void* q_i8,
                          const void* sq, const void* k_i8, const void* sk, const void* v_i8,
                          const void* sv, const void* LD, const void* q_bf, const void* k_bf,
-                         const void* dO_bf, void* dq, void* dk, void* dv, long bh, long seq,
-                         float qks, float sms, hipStream_t st) {
+                         const void* dO_bf, void* dq, void* dk, void* dv, long bh, long sqt, long skt,
+                         int group, int causal, float qks, float sms, hipStream_t st) {
+  const long bkv = bh / group, ny = group * sqt;
   // dV: own K (x8a) / streamed Q8 (y8a), dO image (ytr), LD; scales: sk|sv own, sq|sdO streamed
   if (which & 1)
-    launch_bwd<D, ROLE_DV>(k_i8, nullptr, sk, sv, q_i8, nullptr, dO_bf, nullptr, LD, sq, sdO, nullptr,
-                           dv, nullptr, bh, seq, qks, sms, st);
+    launch_bwd<D, ROLE_DV>(causal, k_i8, nullptr, sk, sv, q_i8, nullptr, dO_bf, nullptr, LD, sq, sdO,
+                           nullptr, dv, nullptr, bkv, skt, ny, 1, sqt, qks, sms, st);
   // dK: own K, V / streamed Q8, dO8, q image, LD
   if (which & 4)
-    launch_bwd<D, ROLE_DK>(k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, nullptr, LD, sq, sdO, nullptr, dk,
-                           nullptr, bh, seq, qks, sms, st);
+    launch_bwd<D, ROLE_DK>(causal, k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, nullptr, LD, sq, sdO, nullptr,
+                           dk, nullptr, bkv, skt, ny, 1, sqt, qks, sms, st);
   // dK and dV in one pass: + dO image
   if (which & 8)
-    launch_bwd<D, ROLE_DKV>(k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, dO_bf, LD, sq, sdO, nullptr, dk,
-                            dv, bh, seq, qks, sms, st);
+    launch_bwd<D, ROLE_DKV>(causal, k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, dO_bf, LD, sq, sdO, nullptr,
+                            dk, dv, bkv, skt, ny, 1, sqt, qks, sms, st);
   // dQ: own Q, dO (+ their LD row stats) / streamed K8, V8, k image; scales: sq|sdO own, sk|sv
   if (which & 2)
-    launch_bwd<D, ROLE_DQ>(q_i8, dO_i8, sq, sdO, k_i8, v_i8, k_bf, nullptr, nullptr, sk, sv, LD, dq,
-                           nullptr, bh, seq, qks, sms, st);
+    launch_bwd<D, ROLE_DQ>(causal, q_i8, dO_i8, sq, sdO, k_i8, v_i8, k_bf, nullptr, nullptr, sk, sv, LD,
+                           dq, nullptr, bh, sqt, skt, group, skt, qks, sms, st);
 }
 
 static int int8_bwd_launch(int which, const void* dO_i8, const void* sdO, const void* q_i8,
                            const void* sq, const void* k_i8, const void* sk, const void* v_i8,
                            const void* sv, const void* LD, const void* q_bf, const void* k_bf,
-                           const void* dO_bf, void* dq, void* dk, void* dv, long bh, long seq,
-                           int head_dim, float qks, float sms, void* stream) {
-  if (seq % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  if (bh == 0 || seq == 0) return 0;
+                           const void* dO_bf, void* dq, void* dk, void* dv, long bh, long sqt,
+                           long skt, int group, int causal, int head_dim, float qks, float sms,
+                           void* stream) {
+  if (sqt % 32 != 0 || skt % 32 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128))
+    return 1;
+  if (bh == 0 || sqt == 0 || skt == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (head_dim == 128)
     bwd_launch_d<128>(which, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
-                      dv, bh, seq, qks, sms, st);
+                      dv, bh, sqt, skt, group, causal, qks, sms, st);
   else
     bwd_launch_d<64>(which, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
-                     dv, bh, seq, qks, sms, st);
+                     dv, bh, sqt, skt, group, causal, qks, sms, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_int8_attn_bwd_ex(const void* dO_i8, const void* sdO, const void* q_i8,
+                                      const void* sq, const void* k_i8, const void* sk,
+                                      const void* v_i8, const void* sv, const void* LD,
+                                      const void* q_bf, const void* k_bf, const void* dO_bf, void* dq,
+                                      void* dk, void* dv, long bh, long sq_tok, long sk_tok, int group,
+                                      int causal, int head_dim, float qks, float sms, void* stream) {
+  return int8_bwd_launch(8 | 2, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
+                         dv, bh, sq_tok, sk_tok, group, causal, head_dim, qks, sms, stream);
 }
 
 extern "C" int qattn_int8_attn_bwd(const void* dO_i8, const void* sdO, const void* q_i8,
@@ -614,7 +655,7 @@ extern "C" int qattn_int8_attn_bwd(const void* dO_i8, const void* sdO, const voi
                                    const void* dO_bf, void* dq, void* dk, void* dv, long bh, long seq,
                                    int head_dim, float qks, float sms, void* stream) {
   return int8_bwd_launch(8 | 2, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
-                         dv, bh, seq, head_dim, qks, sms, stream);
+                         dv, bh, seq, seq, 1, 0, head_dim, qks, sms, stream);
 }
 extern "C" int qattn_int8_bwd_dkdv(const void* dO_i8, const void* sdO, const void* q_i8,
                                    const void* sq, const void* k_i8, const void* sk, const void* v_i8,
@@ -622,7 +663,7 @@ extern "C" int qattn_int8_bwd_dkdv(const void* dO_i8, const void* sdO, const voi
                                    void* dk, void* dv, long bh, long seq, int head_dim, float qks,
                                    float sms, void* stream) {
   return int8_bwd_launch(8, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, nullptr, dO_bf,
-                         nullptr, dk, dv, bh, seq, head_dim, qks, sms, stream);
+                         nullptr, dk, dv, bh, seq, seq, 1, 0, head_dim, qks, sms, stream);
 }
 extern "C" int qattn_int8_bwd_dv(const void* dO_i8, const void* sdO, const void* q_i8,
                                    const void* sq, const void* k_i8, const void* sk, const void* v_i8,
@@ -630,7 +671,7 @@ extern "C" int qattn_int8_bwd_dv(const void* dO_i8, const void* sdO, const void*
                                    void* dk, void* dv, long bh, long seq, int head_dim, float qks,
                                    float sms, void* stream) {
   return int8_bwd_launch(1, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, nullptr, dO_bf,
-                         nullptr, dk, dv, bh, seq, head_dim, qks, sms, stream);
+                         nullptr, dk, dv, bh, seq, seq, 1, 0, head_dim, qks, sms, stream);
 }
 extern "C" int qattn_int8_bwd_dk(const void* dO_i8, const void* sdO, const void* q_i8,
                                    const void* sq, const void* k_i8, const void* sk, const void* v_i8,
@@ -638,12 +679,12 @@ extern "C" int qattn_int8_bwd_dk(const void* dO_i8, const void* sdO, const void*
                                    void* dk, void* dv, long bh, long seq, int head_dim, float qks,
                                    float sms, void* stream) {
   return int8_bwd_launch(4, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, nullptr, dO_bf,
-                         nullptr, dk, dv, bh, seq, head_dim, qks, sms, stream);
+                         nullptr, dk, dv, bh, seq, seq, 1, 0, head_dim, qks, sms, stream);
 }
 extern "C" int qattn_int8_bwd_dq(const void* dO_i8, const void* sdO, const void* q_i8,
                                  const void* sq, const void* k_i8, const void* sk, const void* v_i8,
                                  const void* sv, const void* LD, const void* k_bf, void* dq, long bh,
                                  long seq, int head_dim, float qks, float sms, void* stream) {
   return int8_bwd_launch(2, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, nullptr, k_bf, nullptr, dq,
-                         nullptr, nullptr, bh, seq, head_dim, qks, sms, stream);
+                         nullptr, nullptr, bh, seq, seq, 1, 0, head_dim, qks, sms, stream);
 }

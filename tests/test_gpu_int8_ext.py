@@ -1,0 +1,110 @@
+"""int8 path with the generalised shapes of SURVEY §8f N2 (extensions with no reference
+counterpart): grouped-query attention (Hq a multiple of Hkv), Sq != Sk and causal masking, against
+the oracle's restatement of the same extension (oracle/restate.py int8_fwd / int8_bwd).
+
+Tolerances as tests/test_gpu_int8.py: quantisation bit-exact; O max-abs <= 1e-2 (causal: 5e-2 on
+the first 32 rows, which keep fewer than 32 keys); lse <= 2 fp16 ulp (+1e-3); grads relL2 <= 0.05
+vs the oracle.  Parity with the reference is not defined here (the
+reference has no such shapes): the oracle pins the documented semantics.
+"""
+import pytest
+import torch
+
+from oracle import restate as R
+
+pytestmark = pytest.mark.gpu
+
+# (B, Hq, Hkv, Sq, Sk, D)
+SHAPES = [(1, 4, 2, 128, 96, 64), (2, 4, 1, 64, 160, 128), (1, 2, 2, 160, 128, 128),
+          (1, 2, 2, 128, 128, 64)]
+
+
+def _inputs(shape, seed=0):
+    B, Hq, Hkv, Sq, Sk, D = shape
+    g = torch.Generator().manual_seed(seed)
+    q = torch.randn((B, Hq, Sq, D), generator=g).half()
+    k = torch.randn((B, Hkv, Sk, D), generator=g).half()
+    v = torch.randn((B, Hkv, Sk, D), generator=g).half()
+    return q, k, v
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("causal", [False, True])
+def test_int8_fwd_gqa_causal(lib, shape, causal):
+    from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
+    q, k, v = _inputs(shape, seed=1)
+    ref = R.int8_fwd(q, k, v, causal=causal)
+    out = helion_atten_int8_hl_dot_fwd(q.cuda(), k.cuda(), v.cuda(), causal=causal)
+    torch.cuda.synchronize()
+    for i in (2, 3, 4, 5, 6, 7):
+        assert out[i].shape == ref[i].shape and torch.equal(out[i].cpu(), ref[i]), i
+    assert out[0].shape == ref[0].shape
+    diff = (out[0].float().cpu() - ref[0].float()).abs()
+    if causal:
+        # rows that keep fewer than 32 keys: one P_i8 = trunc(127 e) step -- where the kernel's f16
+        # exponential and the oracle's fp32 one straddle an integer -- moves O by |v|/127 divided by
+        # a row sum of only a few terms, so these rows get 5e-2; every other row the 1e-2 bar
+        assert diff[:, :, :32].max().item() <= 5e-2, diff[:, :, :32].max().item()
+        diff = diff[:, :, 32:]
+    err = diff.max().item()
+    assert err <= 1e-2, err
+    lerr = (out[1].float().cpu() - ref[1].float()).abs()
+    assert (lerr <= 2 * 2.0 ** -10 * ref[1].float().abs() + 1e-3).all(), lerr.max().item()
+
+
+def test_int8_causal_first_row_is_first_value(lib):
+    """Causal row 0 keeps key 0 only: O[0] is the dequantised v[0] = v_i8[0] * sv (P_i8 = 127,
+    sp = 1/127), up to the fp16 roundings of the two P.V operands."""
+    from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
+    q, k, v = _inputs((1, 2, 2, 64, 64, 64), seed=2)
+    out = helion_atten_int8_hl_dot_fwd(q.cuda(), k.cuda(), v.cuda(), causal=True)
+    O = out[0].float().cpu()
+    vi, sv = out[4].cpu().view(2, 64, 64), out[7].float().cpu().view(2, 2)
+    vdq0 = vi[:, 0].float() * sv[:, 0:1]                  # head h, row 0, block 0 scale
+    assert (O[0, :, 0] - vdq0).abs().max().item() <= 2e-3 * max(1.0, vdq0.abs().max().item())
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("causal", [False, True])
+def test_int8_bwd_gqa_causal(lib, shape, causal):
+    from quantizedattention_amd.attention_int8 import (helion_atten_int8_hl_dot_bwd,
+                                                       helion_atten_int8_hl_dot_fwd)
+    B, Hq, Hkv, Sq, Sk, D = shape
+    q, k, v = _inputs(shape, seed=3)
+    dO = torch.randn((B, Hq, Sq, D), generator=torch.Generator().manual_seed(4)).half()
+    O, lse, qi, kiT, vi, sq, sk, sv, Bq, Bkv = helion_atten_int8_hl_dot_fwd(
+        q.cuda(), k.cuda(), v.cuda(), causal=causal)
+    dq, dk, dv = helion_atten_int8_hl_dot_bwd(dO.cuda(), qi, sq, kiT, None, sk, vi, sv, O, lse, Bq, Bkv,
+                                              causal=causal, kv_heads=Hkv)
+    torch.cuda.synchronize()
+    rq, rk, rv = R.int8_bwd(dO, qi.cpu(), sq.cpu(), kiT.cpu(), None, sk.cpu(), vi.cpu(), sv.cpu(),
+                            O.cpu(), lse.cpu(), causal=causal, kv_heads=Hkv)
+    assert dq.shape == (B, Hq, Sq, D) and dk.shape == (B, Hkv, Sk, D) and dv.shape == dk.shape
+    for name, a, b in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
+        assert torch.isfinite(a).all(), name
+        assert _rel(a.cpu(), b) <= 0.05, (name, _rel(a.cpu(), b))
+
+
+def test_int8_autograd_gqa_causal(lib):
+    """sage_attention_3_int8(..., causal=True) through autograd with 4 query heads per key/value
+    head: grads land on the leaves with their own shapes and match the composed oracle."""
+    from quantizedattention_amd.attention_int8 import sage_attention_3_int8
+    shape = (1, 4, 1, 96, 128, 64)
+    q, k, v = _inputs(shape, seed=5)
+    qc, kc, vc = (t.cuda().requires_grad_() for t in (q, k, v))
+    O = sage_attention_3_int8(qc, kc, vc, causal=True)
+    dO = torch.randn(O.shape, generator=torch.Generator().manual_seed(6)).half()
+    O.backward(dO.cuda())
+    assert qc.grad.shape == q.shape and kc.grad.shape == k.shape and vc.grad.shape == v.shape
+    ks, km = R.k_smooth(k)
+    ref = R.int8_fwd(q, ks, v, causal=True)
+    diff = (O.detach().float().cpu() - ref[0].float()).abs()
+    assert diff[:, :, :32].max().item() <= 5e-2 and diff[:, :, 32:].max().item() <= 1e-2
+    rq, rk, rv = R.int8_bwd(dO, ref[2], ref[5], ref[3], km, ref[6], ref[4], ref[7], ref[0], ref[1],
+                            causal=True)
+    for name, a, b in (("dq", qc.grad, rq), ("dk", kc.grad, rk), ("dv", vc.grad, rv)):
+        assert _rel(a.cpu(), b) <= 0.05, (name, _rel(a.cpu(), b))
