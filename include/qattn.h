@@ -46,6 +46,11 @@ int qattn_int8_quant_img(const void* x, void* idx, void* scale, void* deq, void*
                          const void* kmean, long rows, int rows_per_head, int head_dim,
                          void* stream);
 
+/* deq = f16(idx * s) with s the block scale of each 32-row block (rows % 32 == 0): the quantiser's
+ * deq output rebuilt from stored indices and scales (the int8 key/value cache of kv_cache.py). */
+int qattn_int8_dequant(const void* idx, const void* scale, void* deq, long rows, int head_dim,
+                       void* stream);
+
 /* k_mean = f16(mean over the S tokens of each head) — k f16 [bh*seq, D] -> kmean f16 [bh, D]
  * (SageAttention smoothing; replaces the crashing `k.mean(0)` of attention_int8.py:24-25). */
 int qattn_kmean(const void* k, void* kmean, long bh, long seq, int head_dim, void* stream);

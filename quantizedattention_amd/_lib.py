@@ -24,6 +24,7 @@ _vp = ctypes.c_void_p
 SIGNATURES = {
     "qattn_int8_quant": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_int, _c_int, _vp],
     "qattn_int8_quant_img": [_vp] * 6 + [_c_long, _c_int, _c_int, _vp],
+    "qattn_int8_dequant": [_vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_int8_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],

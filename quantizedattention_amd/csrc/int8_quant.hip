@@ -167,3 +167,35 @@ extern "C" int qattn_kmean(const void* k, void* kmean, long bh, long seq, int he
                        (_Float16*)kmean, (int)seq);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// ------------------------------------------------------------------------- dequantised image
+// deq = f16(idx * s) per 32-row block, exactly the DEQ output of the quantiser: rebuilds the P.V
+// operand of a key/value cache restored from its int8 wire format (kv_cache.py).
+// 8 elements per thread.
+__global__ __launch_bounds__(256) void int8_dequant_kernel(const int8_t* __restrict__ idx,
+                                                           const _Float16* __restrict__ scale,
+                                                           _Float16* __restrict__ deq, long n8,
+                                                           int block_elems) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const float s = (float)scale[(i * 8) / block_elems];
+  const v2u w = reinterpret_cast<const v2u*>(idx)[i];
+  v8h o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int q = (int)(signed char)((w[j >> 2] >> (8 * (j & 3))) & 0xff);
+    o[j] = (_Float16)((float)q * s);
+  }
+  reinterpret_cast<v8h*>(deq)[i] = o;
+}
+
+extern "C" int qattn_int8_dequant(const void* idx, const void* scale, void* deq, long rows,
+                                  int head_dim, void* stream) {
+  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  const long n8 = rows * head_dim / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(int8_dequant_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const int8_t*)idx, (const _Float16*)scale, (_Float16*)deq,
+                     n8, 32 * head_dim);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -1,0 +1,91 @@
+"""int8 key/value cache: wire format on the CPU, cached attention on the GPU.
+
+GPU parity: the cached forward is bit-identical to helion_atten_int8_hl_dot_fwd on the un-cached
+tensors (same quantiser, same kernel); appended blocks are bit-identical to quantising the whole
+sequence; the rebuilt P.V operand equals the quantiser's own output bit for bit.
+"""
+import pytest
+import torch
+
+from quantizedattention_amd.kv_cache import MAGIC, QuantizedKV
+
+
+def _random_cache(B=2, H=3, S=64, D=64, smoothed=True, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    k = torch.randint(-127, 128, (B, H, S, D), generator=g, dtype=torch.int8)
+    v = torch.randint(-127, 128, (B, H, S, D), generator=g, dtype=torch.int8)
+    sk = torch.rand(B * H * S // 32, generator=g).half()
+    sv = torch.rand(B * H * S // 32, generator=g).half()
+    km = torch.randn(B, H, 1, D, generator=g).half() if smoothed else None
+    return QuantizedKV(k, v, sk, sv, km)
+
+
+@pytest.mark.parametrize("smoothed", [False, True])
+def test_wire_format_round_trip(smoothed):
+    kv = _random_cache(smoothed=smoothed)
+    buf = kv.to_bytes()
+    assert buf.dtype == torch.uint8 and bytes(buf[:8].tolist()) == MAGIC
+    back = QuantizedKV.from_bytes(buf)
+    for name in ("k_i8", "v_i8", "sk", "sv"):
+        assert torch.equal(getattr(back, name), getattr(kv, name)), name
+    assert (back.k_mean is None) == (not smoothed)
+    if smoothed:
+        assert torch.equal(back.k_mean, kv.k_mean)
+
+
+def test_wire_format_rejects_garbage():
+    from quantizedattention_amd import _lib
+    with pytest.raises(_lib.QAttnError, match="magic"):
+        QuantizedKV.from_bytes(torch.zeros(64, dtype=torch.uint8))
+
+
+def _fp16(shape, seed):
+    return torch.randn(shape, generator=torch.Generator().manual_seed(seed)).half()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hq,hkv,causal", [(4, 4, False), (4, 2, True), (8, 1, False)])
+def test_cached_attention_matches_forward(lib, hq, hkv, causal):
+    from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
+    from quantizedattention_amd.kv_cache import attention_int8_cached, quantize_kv
+    q = _fp16((1, hq, 96, 128), 1).cuda()
+    k = _fp16((1, hkv, 160, 128), 2).cuda()
+    v = _fp16((1, hkv, 160, 128), 3).cuda()
+    ref = helion_atten_int8_hl_dot_fwd(q, k, v, causal=causal)
+    kv = quantize_kv(k, v, smooth=False)
+    kv2 = QuantizedKV.from_bytes(kv.to_bytes().cpu(), device="cuda")   # through the wire format
+    O, lse = attention_int8_cached(q, kv2, causal=causal)
+    torch.cuda.synchronize()
+    assert torch.equal(O, ref[0]) and torch.equal(lse, ref[1])
+    assert torch.equal(kv2.k_i8.view(-1, 128), ref[3].t()) and torch.equal(kv2.sk, ref[6])
+
+
+@pytest.mark.gpu
+def test_cache_append_and_vdq(lib):
+    from quantizedattention_amd import _lib
+    from quantizedattention_amd.kv_cache import quantize_kv
+    k = _fp16((2, 2, 128, 64), 4).cuda()
+    v = _fp16((2, 2, 128, 64), 5).cuda()
+    whole = quantize_kv(k, v, smooth=False)
+    grown = quantize_kv(k[:, :, :64], v[:, :, :64], smooth=False).append(k[:, :, 64:], v[:, :, 64:])
+    for name in ("k_i8", "v_i8", "sk", "sv"):
+        assert torch.equal(getattr(grown, name), getattr(whole, name)), name
+    # rebuilt f16(v_i8 * sv) == the quantiser's own deq output
+    restored = QuantizedKV.from_bytes(whole.to_bytes())
+    assert restored._vdq is None
+    assert torch.equal(restored.vdq(), whole.vdq())
+    with pytest.raises(_lib.QAttnError):
+        whole.append(k[:, :, :16], v[:, :, :16])
+
+
+@pytest.mark.gpu
+def test_cache_from_forward_outputs(lib):
+    from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
+    from quantizedattention_amd.kv_cache import attention_int8_cached
+    q = _fp16((2, 2, 64, 64), 6).cuda()
+    k = _fp16((2, 2, 64, 64), 7).cuda()
+    v = _fp16((2, 2, 64, 64), 8).cuda()
+    out = helion_atten_int8_hl_dot_fwd(q, k, v)
+    kv = QuantizedKV.from_forward_outputs(out, batch=2, kv_heads=2)
+    O, lse = attention_int8_cached(q, kv)
+    assert torch.equal(O, out[0]) and torch.equal(lse, out[1])
