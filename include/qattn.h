@@ -132,6 +132,11 @@ int qattn_int8_bwd_dq(const void* dO_i8, const void* sdO, const void* q_i8, cons
 int qattn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
                    long sq, long sk, int head_dim, int causal, float qks, void* stream);
 
+/* qattn_bf16_fwd with grouped-query attention: bh = batch * query heads, k and v
+ * have bh / group heads (query head h reads key/value head h / group).  qattn_bf16_fwd is group = 1. */
+int qattn_bf16_fwd_ex(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
+                      long sq, long sk, int group, int causal, int head_dim, float qks, void* stream);
+
 /* Backward prologue, one pass: dO f32 -> dO_bf bf16 [rows, D] and LD f32x2 [rows] =
  * {lse[row], D = rowsum(dO*O)} (attention_bf16.py:416, computed once per row instead of per tile). */
 int qattn_bf16_bwd_prep(const void* dO, const void* O, const void* lse, void* dO_bf, void* LD, long bh,
@@ -148,6 +153,12 @@ int qattn_f16_to_bf16(const void* x, void* y, long n, void* stream);
 int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
                    const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh, long sq,
                    long sk, int head_dim, int causal, float qks, float sms, void* stream);
+
+/* qattn_bf16_bwd for grouped-query attention: dk, dv [bh/group * sk, D] sum over the group of
+ * query heads of their key/value head; q_bf, k_bf as the query / key tensors. */
+int qattn_bf16_bwd_ex(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
+                      const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh, long sq,
+                      long sk, int group, int causal, int head_dim, float qks, float sms, void* stream);
 
 /* ---------------------------------------------------------------- JVP (attention_jvp.py) */
 

@@ -80,6 +80,9 @@ def bf16_fwd(q, k, v, causal=False, kt=16):
     ``kt`` is the k-tile width the beta rule is applied at (reference default unpinned, F8; the
     only pinned config, bf16:736, uses 16).
     """
+    if k.shape[1] != q.shape[1]:   # grouped-query attention (N2 extension): expand k/v heads
+        G = q.shape[1] // k.shape[1]
+        k, v = k.repeat_interleave(G, dim=1), v.repeat_interleave(G, dim=1)
     B, H, S, D = q.shape
     Sk = k.shape[2]
     BH = B * H
@@ -121,6 +124,18 @@ def bf16_fwd(q, k, v, causal=False, kt=16):
 # A3 (build contract): corrected FA2 backward in fp32 (bf16:299-448 with F3 fixed)
 # --------------------------------------------------------------------------------------------
 def bf16_bwd(q, k, v, O, lse, causal, dO):
+    """Grouped-query wrapper (N2 extension): expand k/v to the query heads, sum dk/dv per group."""
+    Hq, Hkv = q.shape[1], k.shape[1]
+    if Hkv == Hq:
+        return _bf16_bwd_heads(q, k, v, O, lse, causal, dO)
+    G = Hq // Hkv
+    dq, dk, dv = _bf16_bwd_heads(q, k.repeat_interleave(G, dim=1), v.repeat_interleave(G, dim=1), O, lse,
+                                 causal, dO)
+    B, _, Sk, D = dk.shape
+    return dq, dk.view(B, Hkv, G, Sk, D).sum(2), dv.view(B, Hkv, G, Sk, D).sum(2)
+
+
+def _bf16_bwd_heads(q, k, v, O, lse, causal, dO):
     """Corrected restatement of helion_flash_atten_2_algo_4_bwd (bf16:309-448).
 
     Same inputs/outputs as the reference (fp32 grads).  Fixes: dS = P*(dP-D) instead of

@@ -38,6 +38,9 @@ SIGNATURES = {
     "qattn_int8_bwd_dk": [_vp] * 13 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_int8_bwd_dq": [_vp] * 11 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_bf16_fwd": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
+    "qattn_bf16_fwd_ex": [_vp] * 5 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
+    "qattn_bf16_bwd_ex": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
+                                        _c_float, _vp],
     "qattn_bf16_bwd_prep": [_vp] * 5 + [_c_long, _c_long, _c_int, _vp],
     "qattn_f16_to_bf16": [_vp, _vp, _c_long, _vp],
     "qattn_bf16_bwd": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],

@@ -8,7 +8,8 @@ Public names (same signatures, outputs and assertion messages):
   baseline_pytorch_attention                attention_bf16.py:450-478
 
 Forward: bf16 FlashAttention with the reference's "multiple-max" beta rule emulated at its pinned
-k-tile of 16 (bf16:736).  Backward: FA2 algorithm 4 with the build-contract fixes of SURVEY F3
+k-tile of 16 (bf16:736).  Extension: k, v may have fewer heads than q (grouped-query
+attention, query head h reads key/value head h // (Hq / Hkv)); dk, dv then sum over each group.  Backward: FA2 algorithm 4 with the build-contract fixes of SURVEY F3
 (dS = P*(dP-D), sm_scale, deterministic dQ).
 """
 from __future__ import annotations
@@ -42,8 +43,8 @@ def _check(q, k, v):
     assert k_tokens == v_tokens, "input k_tokens must match v_tokens"  # bf16:154
     assert q_head_dim == k.size(-1) == v.size(-1), \
         "all head dimensions must match for q, k, v tensors"  # bf16:155
-    if not (q.shape[:2] == k.shape[:2] == v.shape[:2]):
-        raise _lib.QAttnError("qattn bf16: batch/head dims of q, k, v must match")
+    if not (q.shape[0] == k.shape[0] and k.shape[:2] == v.shape[:2] and head % k.shape[1] == 0):
+        raise _lib.QAttnError("qattn bf16: batch must match and q heads must be a multiple of k/v heads")
     if q_tokens % 32 or k_tokens % 32:
         raise _lib.QAttnError("qattn bf16: token counts must be multiples of 32")
     if q_head_dim not in (64, 128):
@@ -67,8 +68,9 @@ def helion_atten_bf16_fwd_training(
     O = torch.empty((B, H, S, D), dtype=torch.float32, device=q.device)
     lse = torch.empty((B * H, S), dtype=torch.float32, device=q.device)
     qks = _f32(1.0 / math.sqrt(D) * 1.44269504)
-    _lib.call("qattn_bf16_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(O), _lib.ptr(lse),
-              B * H, S, Sk, D, int(bool(causal)), qks, _lib.stream_of(q))
+    # grouped-query attention (SURVEY §8f N2 extension): query head h reads k/v head h // (H / Hkv)
+    _lib.call("qattn_bf16_fwd_ex", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(O), _lib.ptr(lse),
+              B * H, S, Sk, H // k.shape[1], int(bool(causal)), D, qks, _lib.stream_of(q))
     return O, lse
 
 
@@ -103,13 +105,14 @@ def helion_flash_atten_2_algo_4_bwd(
     _lib.call("qattn_f16_to_bf16", _lib.ptr(q), _lib.ptr(q_bf), q.numel(), st)
     _lib.call("qattn_f16_to_bf16", _lib.ptr(k), _lib.ptr(k_bf), k.numel(), st)
     dq = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
-    dk = torch.empty((B, H, Sk, D), dtype=torch.float32, device=dev)
-    dv = torch.empty((B, H, Sk, D), dtype=torch.float32, device=dev)
+    Hkv = k.shape[1]
+    dk = torch.empty((B, Hkv, Sk, D), dtype=torch.float32, device=dev)
+    dv = torch.empty((B, Hkv, Sk, D), dtype=torch.float32, device=dev)
     qks = _f32(1.0 / math.sqrt(D) * 1.44269504)
     sms = _f32(1.0 / math.sqrt(D))
-    _lib.call("qattn_bf16_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(LD),
+    _lib.call("qattn_bf16_bwd_ex", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(LD),
               _lib.ptr(q_bf), _lib.ptr(k_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
-              B * H, S, Sk, D, int(bool(causal)), qks, sms, st)
+              B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms, st)
     return dq, dk, dv
 
 

@@ -144,8 +144,8 @@ template <int D, int ROLE, bool CAUSAL>
 __global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void bf16_bwd_kernel(
     const _Float16* __restrict__ xa, const __bf16* __restrict__ xb, const _Float16* __restrict__ ya,
     const __bf16* __restrict__ yb, const __bf16* __restrict__ ytr, const float2* __restrict__ yld,
-    const float2* __restrict__ xld, float* __restrict__ out, int BH, int Sx, int Sy, float qks,
-    float osc) {
+    const float2* __restrict__ xld, float* __restrict__ out, int BH, int Sx, int Ny, int ydiv, int Smod,
+    float qks, float osc) {
   using G = B16Cfg<D, ROLE>;
   constexpr bool TWO = G::TWO;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -158,18 +158,21 @@ __global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void bf16_
   const int x0 = xt * G::XROWS + wave * 32;
   const bool active = x0 < Sx;
   const int xi = x0 + c32;                      // this lane's own row
-  const long hx = (long)bh * Sx, hy = (long)bh * Sy;
+  // own head bh streams the Ny rows from (bh / ydiv) * Ny: dV/dK the G query heads of a key/value
+  // head (contiguous, Ny = G * Sq), dQ the key/value head of a query head (ydiv = G, Ny = Sk);
+  // positions of streamed rows are taken mod Smod
+  const long hx = (long)bh * Sx, hy = (long)(bh / ydiv) * Ny;
   // tile range: causal tiles masked for the whole workgroup are skipped (they contribute
   // exp2(-128 - lse) < 2^-120 per element)
-  int t0 = 0, t1 = Sy / 32;
+  int t0 = 0, t1 = Ny / 32;
   if (CAUSAL) {
     if (ROLE == B16_DQ) t1 = min(t1, (xt * G::XROWS + G::XROWS) / 32);   // keys >= every query
-    else t0 = min(t1, (xt * G::XROWS) / 32);                               // queries <= every key
+    else if (Ny == Smod) t0 = min(t1, (xt * G::XROWS) / 32);              // queries <= every key
   }
   const int nt = t1 - t0;
 
   B16Dma<D, ROLE> dma;
-  dma.init(wave, lane, Sy, reinterpret_cast<const char*>(ya + hy * D),
+  dma.init(wave, lane, Ny, reinterpret_cast<const char*>(ya + hy * D),
            reinterpret_cast<const char*>(yb + hy * D), reinterpret_cast<const char*>(ytr + hy * D),
            reinterpret_cast<const char*>(yld + hy));
   const unsigned smem_lds = lds_addr(smem);
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void bf16_
   };
   // fp32 P (DV) or dS (DK, DQ) of tile t
   auto values = [&](auto SLc, int t, const v16f& sa, const v16f& pa, float* X) {
-    const int y0 = 32 * t;
+    const int y0 = (32 * t) % Smod;
     const bool mask = CAUSAL && (ROLE == B16_DQ ? (y0 + 31 >= x0) : (y0 <= x0 + 31));
     if constexpr (G::HAS_LD) {
       const float* ld = reinterpret_cast<const float*>(slot(SLc) + G::LDO);
@@ -351,8 +354,8 @@ extern "C" int qattn_f16_to_bf16(const void* x, void* y, long n, void* stream) {
 
 template <int D, int ROLE, bool CAUSAL>
 static void launch_b16c(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
-                        const void* yld, const void* xld, void* out, long bh, long sx, long sy,
-                        float qks, float osc, hipStream_t st) {
+                        const void* yld, const void* xld, void* out, long bh, long sx, long ny,
+                        int ydiv, long smod, float qks, float osc, hipStream_t st) {
   using G = B16Cfg<D, ROLE>;
   hipFuncSetAttribute((const void*)bf16_bwd_kernel<D, ROLE, CAUSAL>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
@@ -360,38 +363,54 @@ static void launch_b16c(const void* xa, const void* xb, const void* ya, const vo
   hipLaunchKernelGGL((bf16_bwd_kernel<D, ROLE, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
                      G::LDS, st, (const _Float16*)xa, (const __bf16*)xb, (const _Float16*)ya,
                      (const __bf16*)yb, (const __bf16*)ytr, (const float2*)yld, (const float2*)xld,
-                     (float*)out, (int)bh, (int)sx, (int)sy, qks, osc);
+                     (float*)out, (int)bh, (int)sx, (int)ny, ydiv, (int)smod, qks, osc);
 }
 template <int D, int ROLE>
 static void launch_b16(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
-                       const void* yld, const void* xld, void* out, long bh, long sx, long sy,
-                       int causal, float qks, float osc, hipStream_t st) {
-  if (causal) launch_b16c<D, ROLE, true>(xa, xb, ya, yb, ytr, yld, xld, out, bh, sx, sy, qks, osc, st);
-  else launch_b16c<D, ROLE, false>(xa, xb, ya, yb, ytr, yld, xld, out, bh, sx, sy, qks, osc, st);
+                       const void* yld, const void* xld, void* out, long bh, long sx, long ny,
+                       int ydiv, long smod, int causal, float qks, float osc, hipStream_t st) {
+  if (causal)
+    launch_b16c<D, ROLE, true>(xa, xb, ya, yb, ytr, yld, xld, out, bh, sx, ny, ydiv, smod, qks, osc, st);
+  else
+    launch_b16c<D, ROLE, false>(xa, xb, ya, yb, ytr, yld, xld, out, bh, sx, ny, ydiv, smod, qks, osc, st);
 }
 
+// bh = batch * query heads; key/value tensors have bh / group heads of sk rows
 template <int D>
 static void bf16_bwd_d(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
                        const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh,
-                       long sq, long sk, int causal, float qks, float sms, hipStream_t st) {
+                       long sq, long sk, int group, int causal, float qks, float sms, hipStream_t st) {
+  const long bkv = bh / group, ny = group * sq;
   // dV: own K / streamed Q rows, dO tr image, LD
-  launch_b16<D, B16_DV>(k, nullptr, q, nullptr, dO_bf, LD, nullptr, dv, bh, sk, sq, causal, qks, 1.0f, st);
+  launch_b16<D, B16_DV>(k, nullptr, q, nullptr, dO_bf, LD, nullptr, dv, bkv, sk, ny, 1, sq, causal, qks,
+                        1.0f, st);
   // dK: own K, V / streamed Q rows, dO rows, Q bf16 tr image, LD
-  launch_b16<D, B16_DK>(k, v, q, dO_bf, q_bf, LD, nullptr, dk, bh, sk, sq, causal, qks, sms, st);
+  launch_b16<D, B16_DK>(k, v, q, dO_bf, q_bf, LD, nullptr, dk, bkv, sk, ny, 1, sq, causal, qks, sms, st);
   // dQ: own Q, dO (+ LD of their rows) / streamed K rows, V rows, K bf16 tr image
-  launch_b16<D, B16_DQ>(q, dO_bf, k, v, k_bf, nullptr, LD, dq, bh, sq, sk, causal, qks, sms, st);
+  launch_b16<D, B16_DQ>(q, dO_bf, k, v, k_bf, nullptr, LD, dq, bh, sq, sk, group, sk, causal, qks, sms,
+                        st);
+}
+
+extern "C" int qattn_bf16_bwd_ex(const void* q, const void* k, const void* v, const void* dO_bf,
+                                 const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
+                                 void* dv, long bh, long sq, long sk, int group, int causal,
+                                 int head_dim, float qks, float sms, void* stream) {
+  if (sq % 32 != 0 || sk % 32 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128))
+    return 1;
+  if (bh == 0 || sq == 0 || sk == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (head_dim == 128)
+    bf16_bwd_d<128>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, qks, sms, st);
+  else
+    bf16_bwd_d<64>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, qks, sms, st);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 extern "C" int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf,
                               const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
                               void* dv, long bh, long sq, long sk, int head_dim, int causal, float qks,
                               float sms, void* stream) {
-  if (sq % 32 != 0 || sk % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  if (bh == 0 || sq == 0 || sk == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  if (head_dim == 128)
-    bf16_bwd_d<128>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, causal, qks, sms, st);
-  else
-    bf16_bwd_d<64>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, causal, qks, sms, st);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
+  return qattn_bf16_bwd_ex(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, 1, causal, head_dim,
+                           qks, sms, stream);
 }

@@ -104,7 +104,7 @@ QA_DEVICE float rne1(float a) { return __uint_as_float(pk_bf16(a, a) & 0xffff000
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void bf16_fwd_kernel(
     const _Float16* __restrict__ q, const _Float16* __restrict__ k, const __bf16* __restrict__ v,
-    float* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, float qks) {
+    float* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks) {
   using C = Bf16FwdCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nq = (Sq + C::QROWS - 1) / C::QROWS;
@@ -120,7 +120,8 @@ __global__ __launch_bounds__(256, 2) void bf16_fwd_kernel(
   const int nt = Sk / C::KT;
 
   Bf16Dma<D> dma;
-  dma.init(wave, lane, Sk, k + (long)bh * Sk * D, v + (long)bh * Sk * D);
+  // grouped-query attention: query head bh reads key/value head bh / G
+  dma.init(wave, lane, Sk, k + (long)(bh / G) * Sk * D, v + (long)(bh / G) * Sk * D);
   const unsigned smem_lds = lds_addr(smem);
 #pragma unroll
   for (int i = 0; i < C::NSLOT - 1; ++i) dma.issue(smem_lds + i * C::SLOT, min(i, nt - 1));
@@ -344,9 +345,12 @@ __global__ __launch_bounds__(256, 2) void bf16_fwd_kernel(
 
 using namespace qattn;
 
-extern "C" int qattn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
-                              long sq, long sk, int head_dim, int causal, float qks, void* stream) {
-  if (sq % 32 != 0 || sk % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+extern "C" int qattn_bf16_fwd_ex(const void* q, const void* k, const void* v, void* out, void* lse,
+                                 long bh, long sq, long sk, int group, int causal, int head_dim,
+                                 float qks, void* stream) {
+  if (sq % 32 != 0 || sk % 32 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128))
+    return 1;
   if (bh == 0 || sq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
 #define QA_LAUNCH(Dv, CV)                                                                        \
@@ -357,7 +361,7 @@ extern "C" int qattn_bf16_fwd(const void* q, const void* k, const void* v, void*
                         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);                     \
     hipLaunchKernelGGL((bf16_fwd_kernel<Dv, CV>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), \
                        C::LDS, st, (const _Float16*)q, (const _Float16*)k, (const __bf16*)v,     \
-                       (float*)out, (float*)lse, (int)bh, (int)sq, (int)sk, qks);                \
+                       (float*)out, (float*)lse, (int)bh, (int)sq, (int)sk, group, qks);         \
   }
   if (head_dim == 128) {
     if (causal) QA_LAUNCH(128, true) else QA_LAUNCH(128, false)
@@ -366,4 +370,9 @@ extern "C" int qattn_bf16_fwd(const void* q, const void* k, const void* v, void*
   }
 #undef QA_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
+                              long sq, long sk, int head_dim, int causal, float qks, void* stream) {
+  return qattn_bf16_fwd_ex(q, k, v, out, lse, bh, sq, sk, 1, causal, head_dim, qks, stream);
 }

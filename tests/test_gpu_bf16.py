@@ -88,3 +88,28 @@ def test_bf16_autograd_end_to_end(lib):
     torch.nn.functional.mse_loss(ref, gt.cpu()).backward()
     for a, b in ((qd.grad, qf.grad), (kd.grad, kf.grad), (vd.grad, vf.grad)):
         assert _rel(a.float().cpu(), b) <= 3e-2
+
+
+@pytest.mark.parametrize("hq,hkv,sq,sk,causal", [(4, 2, 128, 128, False), (4, 1, 96, 192, True),
+                                                 (6, 2, 128, 64, True)])
+def test_bf16_gqa_fwd_bwd(lib, hq, hkv, sq, sk, causal):
+    """Grouped-query attention (SURVEY §8f N2 extension) vs the oracle on expanded heads: same
+    tolerances as the square tests; dk, dv sum over each group of query heads."""
+    from quantizedattention_amd.attention_bf16 import (helion_atten_bf16_fwd_training,
+                                                       helion_flash_atten_2_algo_4_bwd)
+    g = torch.Generator().manual_seed(31)
+    D = 64
+    q = torch.randn((1, hq, sq, D), generator=g).half()
+    k = torch.randn((1, hkv, sk, D), generator=g).half()
+    v = torch.randn((1, hkv, sk, D), generator=g).bfloat16()
+    dO = torch.randn((1, hq, sq, D), generator=g)
+    O, lse = helion_atten_bf16_fwd_training(q.cuda(), k.cuda(), v.cuda(), causal)
+    O_ref, lse_ref = R.bf16_fwd(q, k, v, causal, kt=16)
+    assert (O.cpu() - O_ref).abs().max().item() <= 5e-3
+    assert (lse.cpu() - lse_ref).abs().max().item() <= 5e-3
+    dq, dk, dv = helion_flash_atten_2_algo_4_bwd(q.cuda(), k.cuda(), v.cuda(), O, lse, causal, dO.cuda())
+    torch.cuda.synchronize()
+    rq, rk, rv = R.bf16_bwd(q, k, v, O.cpu(), lse.cpu(), causal, dO)
+    assert dk.shape == k.shape and dv.shape == v.shape and dq.shape == q.shape
+    for name, a, b in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
+        assert _rel(a.cpu(), b) <= 1e-2, (name, _rel(a.cpu(), b))
