@@ -203,6 +203,13 @@ int qattn_probe_pk(const void* x, void* e, void* t, void* stream);
 int qattn_probe_fwd_helpers(const void* e, const void* sp, void* w, const void* a, const void* cn,
                             void* d, void* stream);
 
+/* MX-FP4 probes: one block-scaled 32x32x64 fp4 MFMA (A, B: 64 lanes x 16 B of e2m1
+ * nibbles, sa / sb: one e8m0 byte per lane, C: 64 x 16 f32) and the scaled fp4 pack/unpack converts
+ * (lane i packs x[8i..8i+7] with scale s[i]). */
+int qattn_probe_mfma_fp4(const void* A, const void* B, const void* sa, const void* sb, void* C,
+                         void* stream);
+int qattn_probe_fp4_cvt(const void* x, const void* s, void* packed, void* back, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

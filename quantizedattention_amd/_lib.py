@@ -52,6 +52,8 @@ SIGNATURES = {
     "qattn_probe_mfma_f16": [_vp, _vp, _vp, _vp],
     "qattn_probe_tr16": [_vp, _vp, _vp],
     "qattn_probe_pk": [_vp, _vp, _vp, _vp],
+    "qattn_probe_mfma_fp4": [_vp] * 6,
+    "qattn_probe_fp4_cvt": [_vp] * 5,
     "qattn_probe_fwd_helpers": [_vp] * 7,
 }
 

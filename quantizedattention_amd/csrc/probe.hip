@@ -111,3 +111,48 @@ extern "C" int qattn_probe_fwd_helpers(const void* e, const void* sp, void* w, c
                      (v2h*)d);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// MX-FP4 probes (layout of the block-scaled MFMA operands and of the fp4 converts):
+//   mfma_fp4: one wave, A / B as 64 lanes x 16 bytes (32 e2m1 nibbles, low nibble first), one
+//   e8m0 scale byte per lane (byte 0 of sa / sb), C = 64 lanes x 16 f32.
+//   fp4_cvt: lane i packs x[8i .. 8i+7] with v_cvt_scalef32_pk_fp4_f32 (scale s[i]) into one dword
+//   and decodes it back with v_cvt_scalef32_pk_f32_fp4 (same scale).
+namespace qattn {
+typedef int v8i_ __attribute__((ext_vector_type(8)));
+__global__ void probe_mfma_fp4_kernel(const v4i* A, const v4i* B, const unsigned* sa, const unsigned* sb,
+                                      v16f* C) {
+  const int l = threadIdx.x;
+  const v4i a4 = A[l], b4 = B[l];
+  const v8i_ a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+  const v8i_ b = {b4[0], b4[1], b4[2], b4[3], 0, 0, 0, 0};
+  C[l] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, v16f{}, 4, 4, 0, (int)sa[l], 0, (int)sb[l]);
+}
+__global__ void probe_fp4_cvt_kernel(const float* x, const float* s, unsigned* packed, float* back) {
+  const int i = threadIdx.x;
+  unsigned w = 0;
+  w = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(w, x[8 * i + 0], x[8 * i + 1], s[i], 0);
+  w = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(w, x[8 * i + 2], x[8 * i + 3], s[i], 1);
+  w = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(w, x[8 * i + 4], x[8 * i + 5], s[i], 2);
+  w = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(w, x[8 * i + 6], x[8 * i + 7], s[i], 3);
+  packed[i] = w;
+#define QA_BACK(j)                                                          \
+  {                                                                         \
+    const auto r = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(w, s[i], j);    \
+    back[8 * i + 2 * j] = r[0];                                             \
+    back[8 * i + 2 * j + 1] = r[1];                                         \
+  }
+  QA_BACK(0) QA_BACK(1) QA_BACK(2) QA_BACK(3)
+#undef QA_BACK
+}
+}  // namespace qattn
+extern "C" int qattn_probe_mfma_fp4(const void* A, const void* B, const void* sa, const void* sb, void* C,
+                                    void* stream) {
+  hipLaunchKernelGGL(probe_mfma_fp4_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const v4i*)A,
+                     (const v4i*)B, (const unsigned*)sa, (const unsigned*)sb, (v16f*)C);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+extern "C" int qattn_probe_fp4_cvt(const void* x, const void* s, void* packed, void* back, void* stream) {
+  hipLaunchKernelGGL(probe_fp4_cvt_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const float*)x,
+                     (const float*)s, (unsigned*)packed, (float*)back);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
