@@ -184,6 +184,27 @@ int qattn_jvp_fwd_x3(const void* q_hi, const void* q_lo, const void* k_hi, const
 /* hi = bf16(x), lo = bf16(x - hi) (both round-to-nearest-even) for n fp32 elements, n % 4 == 0. */
 int qattn_split_bf16(const void* x, void* hi, void* lo, long n, void* stream);
 
+/* ---------------------------------------------------------------- MX-FP4 inference forward
+ * SURVEY §8f N4 (SageAttention3's FP4 path, named in the reference README.md:49-55, not implemented
+ * there: no reference interface is replaced).  OCP MX e2m1 with one e8m0 scale per 32 elements,
+ * e = floor(log2 amax) - 2, code = RNE(sat(x / 2^e)); layouts in csrc/mxfp4_attn.hip. */
+
+/* Q / K rows: x f16 [rows, head_dim] -> q4 u8 [rows, head_dim/2] (low nibble first), scale u8
+ * [rows, head_dim/32].  head_dim 64 or 128. */
+int qattn_mxfp4_quant_rows(const void* x, void* q4, void* scale, long rows, int head_dim, void* stream);
+
+/* V: v f16 [bh*seq, head_dim] -> vt u8 [bh][seq/64][head_dim][32] (operand-ordered keys), vscale u8
+ * [bh][seq/64][head_dim][2].  seq % 64 == 0. */
+int qattn_mxfp4_quant_vt(const void* v, void* vt, void* vscale, long bh, long seq, int head_dim,
+                         void* stream);
+
+/* O f16 [bh*sq, 128] = softmax2(S * qks) V with S from the fp4 Q/K, P re-quantised to fp4 per
+ * 32 keys, l from the fp32 P; lse f32 [bh*sq] (base 2).  Query head h reads key/value head h/group.
+ * sq % 32 == 0, sk % 64 == 0, head_dim 128. */
+int qattn_mxfp4_attn_fwd(const void* q4, const void* qscale, const void* k4, const void* kscale,
+                         const void* vt, const void* vscale, void* out, void* lse, long bh, long sq,
+                         long sk, int group, int head_dim, float qks, void* stream);
+
 /* ---------------------------------------------------------------- diagnostics (not product API) */
 
 /* qattn_int8_attn_fwd with parts of the tile pipeline disabled (ab = 0 full, 1 no softmax,
