@@ -35,6 +35,7 @@ from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward 
 
 PEAK_I8 = 256 * 8192 * 2.4e9          # ops/s, dense int8 MFMA (MI355X_MICROARCH: 2x bf16 per clock)
 PEAK_BF16 = 256 * 4096 * 2.4e9        # flop/s, dense bf16/fp16 MFMA
+PEAK_FP4 = 256 * 16384 * 2.4e9        # flop/s, dense MX-FP4 block-scaled MFMA (4x bf16 per clock)
 PEAK_HBM = 8.0e12                     # B/s
 
 
@@ -139,6 +140,26 @@ def int8_kernel_times(q, k, v, dO, n):
     for name in order:  # populate every buffer once in dependency order
         calls[name]()
     return {name: event_time(calls[name], n) for name in order}
+
+
+def mxfp4_fwd_times(q, k, v, n):
+    """SURVEY §8f N4 beside the headline: the MX-FP4 inference forward at the same shape --
+    the attention kernel alone (operands already quantised) and the whole call (k-mean,
+    quantisers, attention)."""
+    from quantizedattention_amd import _lib
+    from quantizedattention_amd.attention_mxfp4 import _qk_scale, mxfp4_attn_fwd
+    B, H, S, D = q.shape
+    O, lse, ops = mxfp4_attn_fwd(q, k, v)
+    st = _lib.stream_of(q)
+
+    def kern():
+        _lib.call("qattn_mxfp4_attn_fwd", *(_lib.ptr(t) for t in ops), _lib.ptr(O), _lib.ptr(lse),
+                  B * H, S, S, 1, D, _qk_scale(D), st)
+    tk = event_time(kern, n)
+    te = event_time(lambda: mxfp4_attn_fwd(q, k, v), n)
+    flop = 4.0 * B * H * S * S * D
+    return {"kernel_ms": tk, "call_ms": te, "kernel_TFLOPs": flop / (tk * 1e-3) / 1e12,
+            "frac_of_fp4_peak": flop / (tk * 1e-3) / PEAK_FP4}
 
 
 def cpu_baseline(S, D, seconds):
@@ -252,6 +273,7 @@ def main():
         "int8_fwd": {"ms": fwd_ms, "TOPS": 4.0 * B * H * S * S * D / (fwd_ms * 1e-3) / 1e12,
                      "frac_of_int8_peak": 4.0 * B * H * S * S * D / (fwd_ms * 1e-3) / PEAK_I8},
         "kernel_ms": kt,
+        "mxfp4_fwd": mxfp4_fwd_times(q, k, v, max(3, a.steps // 2)) if D == 128 else None,
         "roofline": {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": PEAK_I8 / 1e12,
                      "unit": "TFLOP/s", "frac": achieved * 1e12 / PEAK_I8, "traffic": None},
     }

@@ -190,8 +190,10 @@ int qattn_split_bf16(const void* x, void* hi, void* lo, long n, void* stream);
  * e = floor(log2 amax) - 2, code = RNE(sat(x / 2^e)); layouts in csrc/mxfp4_attn.hip. */
 
 /* Q / K rows: x f16 [rows, head_dim] -> q4 u8 [rows, head_dim/2] (low nibble first), scale u8
- * [rows, head_dim/32].  head_dim 64 or 128. */
-int qattn_mxfp4_quant_rows(const void* x, void* q4, void* scale, long rows, int head_dim, void* stream);
+ * [rows, head_dim/32].  mean (f16 [rows/seq, head_dim]) or NULL: when given, row r is first
+ * smoothed to f16(x - mean[r / seq]) (k_mean from qattn_kmean).  head_dim 64 or 128. */
+int qattn_mxfp4_quant_rows(const void* x, const void* mean, void* q4, void* scale, long rows, long seq,
+                           int head_dim, void* stream);
 
 /* V: v f16 [bh*seq, head_dim] -> vt u8 [bh][seq/64][head_dim][32] (operand-ordered keys), vscale u8
  * [bh][seq/64][head_dim][2].  seq % 64 == 0. */

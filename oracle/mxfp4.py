@@ -112,13 +112,15 @@ def deq_vt(vt, vs):
     return out.permute(0, 1, 3, 2).reshape(BH, ng * 64, D)
 
 
-def mxfp4_fwd(q, k, v):
+def mxfp4_fwd(q, k, v, mslack=8.0):
     """q fp16 [B,H,Sq,D], k/v fp16 [B,Hkv,Sk,D] (H % Hkv == 0, Sk % 64 == 0) ->
     (O fp16 [B,H,Sq,D], lse fp32 [B*H, Sq] base 2, (q4, qs, k4, ks, vt, vs)).
 
-    Per 64-key tile t (the kernel's order): S = deq(Q) deq(K)^T; m_t = max(m, rowmax(S * qks));
-    P = exp2(S * qks - m_t) in fp32; l = l * 2^(m - m_t) + sum(P); P is MX-quantised per query row
-    in two blocks of 32 (the keys whose bit 2 is 0 / 1); O = O * 2^(m - m_t) + deq(P) deq(V).
+    Per 64-key tile t (the kernel's order, csrc/mxfp4_attn.hip header): S = deq(Q) deq(K)^T in
+    fp32; if rowmax(fp32(S * qks)) > m + mslack: m' = ceil(that max), O and l scaled by
+    2^(m - m'); P = exp2(fp32(S * qks - m)) (one rounding, the kernel's fma); P is MX-quantised per
+    query row in two blocks of 32 (the keys whose bit 2 is 0 / 1); l += sum(deq P);
+    O += deq(P) deq(V).
     """
     B, H, Sq, D = q.shape
     Hkv, Sk = k.shape[1], k.shape[2]
@@ -132,23 +134,25 @@ def mxfp4_fwd(q, k, v):
     dq = deq_rows(q4, qs).reshape(BH, Sq, D)
     dk = deq_rows(k4, ks).reshape(B * Hkv, Sk, D)[kvh]
     dv = deq_vt(vt, vs)[kvh]
-    m = torch.full((BH, Sq, 1), float("-inf"), dtype=torch.float32)
-    l = torch.zeros((BH, Sq, 1), dtype=torch.float32)
+    m = torch.full((BH, Sq, 1), float("-inf"), dtype=torch.float64)
+    l = torch.zeros((BH, Sq, 1), dtype=torch.float64)
     O = torch.zeros((BH, Sq, D), dtype=torch.float64)
     order = vt_key_order()
     for t in range(Sk // 64):
         k0 = 64 * t
-        S = (dq @ dk[:, k0:k0 + 64].transpose(1, 2)).to(torch.float32) * qks
-        nm = torch.maximum(m, S.amax(-1, keepdim=True))
-        r = torch.exp2(m - nm)
-        m = nm
-        P = torch.exp2(S - nm)                                    # fp32 [BH, Sq, 64]
-        l = l * r + P.sum(-1, keepdim=True)
-        Pb = P[..., order]                                        # [BH, Sq, 2, 32]
-        codes, b = quant_block32(Pb)
+        acc = (dq @ dk[:, k0:k0 + 64].transpose(1, 2)).to(torch.float32)    # MFMA fp32 result
+        mx = (acc * qks).amax(-1, keepdim=True).double()                   # fp32 products
+        raise_ = mx > m + mslack
+        nm = torch.where(raise_, torch.ceil(mx), m)
+        r = torch.where(torch.isinf(m), torch.zeros_like(m), torch.pow(2.0, m - nm))
+        O, l, m = O * r, l * r, nm
+        # fma(acc, qks, -m): the exact value rounded once to fp32
+        P = torch.exp2((acc.double() * qks - m).to(torch.float32))       # fp32 [BH, Sq, 64]
+        codes, b = quant_block32(P[..., order])
         Pd = torch.zeros((BH, Sq, 64), dtype=torch.float64)
         Pd[..., order] = decode(codes) * scale_value(b)[..., None]
-        O = O * r.to(torch.float64) + Pd @ dv[:, k0:k0 + 64]
-    lse = (m + torch.log2(l)).squeeze(-1)
-    Oh = (O / l.to(torch.float64)).to(torch.float16)
+        l = l + Pd.sum(-1, keepdim=True)
+        O = O + Pd @ dv[:, k0:k0 + 64]
+    lse = (m + torch.log2(l)).squeeze(-1).to(torch.float32)
+    Oh = (O / l).to(torch.float16)
     return Oh.view(B, H, Sq, D), lse, (q4, qs, k4, ks, vt, vs)

@@ -47,7 +47,7 @@ SIGNATURES = {
     "qattn_jvp_fwd": [_vp] * 9 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
     "qattn_jvp_fwd_x3": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_split_bf16": [_vp, _vp, _vp, _c_long, _vp],
-    "qattn_mxfp4_quant_rows": [_vp, _vp, _vp, _c_long, _c_int, _vp],
+    "qattn_mxfp4_quant_rows": [_vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_mxfp4_quant_vt": [_vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_mxfp4_attn_fwd": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_ablate": [_vp] * 7 + [_c_long, _c_long, _c_float, _c_int, _vp],

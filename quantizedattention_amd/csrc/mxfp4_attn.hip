@@ -12,9 +12,12 @@
 //         the key order in which a lane holds P after the swapped S^T = K Q^T product.
 //   P   : per query row, one block per lane half: the 32 probabilities the lane holds of a 64-key
 //         tile (same interleaved key set as V's block h), scale from their own max.
-// Attention: S = (deq Q)(deq K)^T exactly (block-scaled fp4 MFMA, fp32 accumulation);
-// P = exp2(S * qks - m) with the online running max m (fp32); l = sum of the fp32 P;
-// O = (deq P_fp4)(deq V) / l (fp16 out); lse = m + log2(l) (fp32, base 2).
+// Attention per 64-key tile: S = (deq Q)(deq K)^T exactly (block-scaled fp4 MFMA, fp32
+// accumulation); m = ceil(rowmax(S * qks)) when that max exceeds the running m by more than 8
+// (else m stays; m starts at -inf), O and l scaled by the exact power of two 2^(m_old - m_new);
+// P = exp2(fma(S, qks, -m)) in fp32 (so P <= 2^8); P_fp4 = MX(P); l += sum(deq P_fp4);
+// O += (deq P_fp4)(deq V).  Out: O / l (fp16), lse = m + log2(l) (fp32, base 2).  Because every
+// rescale is a power of two, the fp4 codes of P do not depend on when m was raised.
 #include "common.h"
 
 namespace qattn {
@@ -47,19 +50,28 @@ QA_DEVICE v4i pack_fp4x32(const float* x, float s) {
 }
 
 // ------------------------------------------------------------------------------ quantisers
-// Q / K: one thread per 32-element block of a row.  x f16 [rows, D] -> q4 [rows, D/2], sc [rows, D/32]
+// Q / K: one thread per 32-element block of a row.  x f16 [rows, D] -> q4 [rows, D/2], sc [rows, D/32].
+// With ``mean`` (f16 [rows/seq, D], SageAttention smoothing) the row is first f16(x - mean[row/seq]).
 template <int D>
 __global__ __launch_bounds__(256) void mx_quant_rows_kernel(const _Float16* __restrict__ x,
+                                                            const _Float16* __restrict__ mean,
                                                             uint8_t* __restrict__ q4,
-                                                            uint8_t* __restrict__ sc, long nblk) {
+                                                            uint8_t* __restrict__ sc, long nblk, long seq) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= nblk) return;
   const v8h* src = reinterpret_cast<const v8h*>(x + i * 32);
+  constexpr int NB = D / 32;
+  const v8h* mu = mean ? reinterpret_cast<const v8h*>(mean + (i / NB / seq) * D + (i % NB) * 32) : nullptr;
   float f[32];
   float amax = 0.f;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const v8h v = src[c];
+    v8h v = src[c];
+    if (mu) {
+      const v8h w = mu[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] - (float)w[j]);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       f[8 * c + j] = (float)v[j];
@@ -118,11 +130,15 @@ struct MxCfg {
   static constexpr int IPW = IPW16 + 2;               // + the two 256-B scale blocks
   static constexpr int NKS = D / 64;                  // 32x32x64 k-steps of S
   static constexpr int NDB = D / 32;
+  static constexpr float MSLACK = 8.f;                // P <= 2^MSLACK between max raises
   static_assert(KS_BYTES <= 256 && VS_BYTES <= 256 && P16 % WAVES == 0, "tile layout");
 };
 
+#ifndef QA_MX_OCC
+#define QA_MX_OCC 2   // min waves per SIMD the register budget is sized for
+#endif
 template <int D>
-__global__ __launch_bounds__(256, 2) void mxfp4_attn_fwd_kernel(
+__global__ __launch_bounds__(256, QA_MX_OCC) void mxfp4_attn_fwd_kernel(
     const uint8_t* __restrict__ q4, const uint8_t* __restrict__ qs, const uint8_t* __restrict__ k4,
     const uint8_t* __restrict__ ks, const uint8_t* __restrict__ vt, const uint8_t* __restrict__ vs,
     _Float16* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks) {
@@ -184,7 +200,7 @@ __global__ __launch_bounds__(256, 2) void mxfp4_attn_fwd_kernel(
   v16f o[C::NDB];
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) o[b] = v16f{};
-  float m = -INFINITY, lpart = 0.f;   // lpart: this lane half's share of the row sum
+  float m = -INFINITY, l = 0.f;   // integer running max (log2 units), sum of the quantised P
 
   vmem_drain();
   __syncthreads();
@@ -209,38 +225,45 @@ __global__ __launch_bounds__(256, 2) void mxfp4_attn_fwd_kernel(
         acc[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc[u], 4, 4, 0, sa, 0, sb);
       }
     }
-    // online softmax over the tile (fp32); the lane holds 32 keys of its query row
-    float x[32];
-    float mx = -INFINITY;
+    // online softmax over the tile (fp32); the lane holds 32 keys of its query row.  m is an
+    // integer (log2 units) raised only when the row max exceeds it by more than MSLACK, so every
+    // rescale is an exact power of two and, between raises, P <= 2^MSLACK needs no rescale at all.
+    float amx = acc[0][0];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        x[16 * u + r] = acc[u][r] * qks;
-        mx = fmaxf(mx, x[16 * u + r]);
-      }
-    mx = fmaxf(mx, xor32_swap(mx, lane));
-    const float nm = fmaxf(m, mx);
-    const float rsc = exp2_f32(m - nm);
-    m = nm;
-    float pmax = 0.f, psum = 0.f;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      x[j] = exp2_f32(x[j] - nm);
-      psum += x[j];
-      pmax = fmaxf(pmax, x[j]);
-    }
-    lpart = lpart * rsc + psum;
-    if (__ballot(rsc != 1.0f)) {
+      for (int r = (u == 0 ? 1 : 0); r < 16; ++r) amx = fmaxf(amx, acc[u][r]);
+    const float lmx = amx * qks;                                  // this lane's max of S * qks
+    const float mx = fmaxf(lmx, xor32_swap(lmx, lane));
+    if (__ballot(mx > m + C::MSLACK)) {
+      const float nm = mx > m + C::MSLACK ? ceilf(mx) : m;
+      const float rsc = m == -INFINITY ? 0.f : __builtin_ldexpf(1.f, (int)(m - nm));
+      m = nm;
+      l *= rsc;
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b)
 #pragma unroll
         for (int i = 0; i < 16; ++i) o[b][i] = o[b][i] * rsc;
     }
+    const float nm = -m;
+    float x[32];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x[16 * u + r] = exp2_f32(__builtin_fmaf(acc[u][r], qks, nm));
+    // the block max is exp2 of the lane's max argument (exp2 and the fma are monotonic)
+    const float pmax = exp2_f32(__builtin_fmaf(amx, qks, nm));
     // P block of this lane half: its 32 values, nibble j = 16u + r
     const unsigned pe = e8m0_of(pmax);
     const v4i pk = pack_fp4x32(x, e8m0_value(pe));
     const v8i_t pb = {pk[0], pk[1], pk[2], pk[3], 0, 0, 0, 0};
+    // row sum of the quantised P on the matrix core: every row of ONES . P^T is the column sum
+    {
+      const v8i_t ones = {0x22222222, 0x22222222, 0x22222222, 0x22222222, 0, 0, 0, 0};   // e2m1 1.0
+      const v16f ts = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones, pb, v16f{}, 4, 4, 0, 127, 0,
+                                                                      (int)pe);
+      l += ts[0];
+    }
     // O^T[d][q] += V^T[d][keys] P^T[keys][q], A = V^T rows d = 32b + c32, k = the half-h key set
 #pragma unroll
     for (int b = 0; b < C::NDB; ++b) {
@@ -254,7 +277,6 @@ __global__ __launch_bounds__(256, 2) void mxfp4_attn_fwd_kernel(
   vmcnt_wait_all();
   __syncthreads();
   if (!active) return;
-  const float l = lpart + xor32_swap(lpart, lane);
   const long row0 = (long)bh * Sq + q0;
   if (h == 0) lse[row0 + c32] = m + log2_f32(l);
   static_assert(C::WAVES * RowTile<D, _Float16>::BYTES <= C::NSLOT * C::SLOT, "staging fits the ring");
@@ -265,18 +287,19 @@ __global__ __launch_bounds__(256, 2) void mxfp4_attn_fwd_kernel(
 
 using namespace qattn;
 
-extern "C" int qattn_mxfp4_quant_rows(const void* x, void* q4, void* scale, long rows, int head_dim,
-                                      void* stream) {
+extern "C" int qattn_mxfp4_quant_rows(const void* x, const void* mean, void* q4, void* scale, long rows,
+                                      long seq, int head_dim, void* stream) {
   if (head_dim != 64 && head_dim != 128) return 1;
+  if (mean && (seq <= 0 || rows % seq != 0)) return 1;
   const long nblk = rows * head_dim / 32;
   if (nblk == 0) return 0;
   dim3 grid((unsigned)((nblk + 255) / 256)), block(256);
   if (head_dim == 128)
     hipLaunchKernelGGL((mx_quant_rows_kernel<128>), grid, block, 0, (hipStream_t)stream,
-                       (const _Float16*)x, (uint8_t*)q4, (uint8_t*)scale, nblk);
+                       (const _Float16*)x, (const _Float16*)mean, (uint8_t*)q4, (uint8_t*)scale, nblk, seq);
   else
     hipLaunchKernelGGL((mx_quant_rows_kernel<64>), grid, block, 0, (hipStream_t)stream,
-                       (const _Float16*)x, (uint8_t*)q4, (uint8_t*)scale, nblk);
+                       (const _Float16*)x, (const _Float16*)mean, (uint8_t*)q4, (uint8_t*)scale, nblk, seq);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

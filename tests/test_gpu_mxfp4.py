@@ -39,6 +39,21 @@ def test_quant_rows_bit_exact(lib):
         assert torch.equal(q4.cpu(), r4), D
 
 
+def test_quant_rows_smoothed_bit_exact(lib):
+    """k smoothing inside the quantiser: rows of head i become f16(k - k_mean[i]) first."""
+    from quantizedattention_amd import _lib
+    from quantizedattention_amd.attention_mxfp4 import mxfp4_quantize_rows
+    g = torch.Generator().manual_seed(5)
+    k = (torch.randn((2, 3, 96, 128), generator=g) + 4.0).half()
+    kc = k.cuda()
+    km = torch.empty((2, 3, 1, 128), dtype=torch.float16, device="cuda")
+    _lib.call("qattn_kmean", _lib.ptr(kc), _lib.ptr(km), 6, 96, 128, _lib.stream_of(kc))
+    q4, sc = mxfp4_quantize_rows(kc, km)
+    ks = (k.float() - km.cpu().float()).half()
+    r4, rs = M.quant_rows(ks.reshape(-1, 128))
+    assert torch.equal(sc.cpu(), rs) and torch.equal(q4.cpu(), r4)
+
+
 def test_quant_v_bit_exact(lib):
     from quantizedattention_amd.attention_mxfp4 import mxfp4_quantize_v
     g = torch.Generator().manual_seed(1)

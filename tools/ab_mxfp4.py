@@ -48,6 +48,6 @@ tk = timed(kernel)
 tq = timed(lambda: (mxfp4_quantize_rows(q), mxfp4_quantize_rows(k), mxfp4_quantize_v(v)))
 te = timed(lambda: mxfp4_attn_fwd(q, k, v))
 flop = 4 * B * H * S * S * D
-print(f"mxfp4 fwd kernel {tk * 1e3:.1f} us = {flop / tk / 1e9:.0f} TFLOP/s "
+print(f"{os.environ.get('QATTN_LIB', 'default')}: mxfp4 fwd kernel {tk * 1e3:.1f} us = {flop / tk / 1e9:.0f} TFLOP/s "
       f"({flop / tk / 1e9 / 10066 * 100:.1f}% of the 10.07 PF dense fp4 peak); "
       f"quantisers {tq * 1e3:.1f} us; end-to-end {te * 1e3:.1f} us", flush=True)
