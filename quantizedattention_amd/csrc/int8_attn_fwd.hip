@@ -307,9 +307,13 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
     exp2_pk4(&st.d[4], &e[4]);
     // row-sum of e: one packed f16 add level (pairs of values <= 1), then fp32; v_dot2c_f32_f16 is
     // avoided: beside MFMAs it issues ~5x slower than plain VALU (tools/ubench)
-    float esum = 0.f;
+    float esum;   // (not 0.f + ...: a float +0 is not folded away)
+    {
+      const v2h p = e[0] + e[1];
+      esum = (float)p[0] + (float)p[1];
+    }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 1; j < 4; ++j) {
       const v2h p = e[2 * j] + e[2 * j + 1];
       esum += (float)p[0] + (float)p[1];
     }

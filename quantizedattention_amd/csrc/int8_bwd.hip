@@ -165,6 +165,13 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #ifndef QA_DKV_PIPE
 #define QA_DKV_PIPE 0
 #endif
+// Stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): the second half of the fused dK+dV
+// workgroup (the second wave on every SIMD) runs the pipelined order, half a tile out of phase with
+// its partner, so the two waves of a SIMD are not in the same phase (MFMA vs VALU) at the same time.
+// Measured 1.5-5 % faster than both waves unpipelined (tools/ab_bwd.py, four boxes).
+#ifndef QA_DKV_STAGGER
+#define QA_DKV_STAGGER 1
+#endif
 
 template <int D, int ROLE>
 struct BwdCfg {
@@ -452,7 +459,7 @@ void int8_bwd_kernel(
         values(tn, sa, pa, X, X);
       }
     }
-  } else if constexpr (QA_DKV_PIPE) {
+  } else if (QA_DKV_PIPE || (QA_DKV_STAGGER && wave >= G::WAVES / 2)) {
     // DKV pipelined: carry the quantised bf16 operands of tile t (16 VGPRs) into iteration t, whose
     // int8 products for tile t+1 are issued first and whose fp32 values of t+1 are computed beside
     // the bf16 MFMAs of tile t
@@ -465,6 +472,9 @@ void int8_bwd_kernel(
       quantise(dS, so_ds(0), opS);
       quantise(P, so_p(0), opP);
     }
+#if QA_DKV_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
     for (int t = 0; t < nt; ++t) {
       ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
       dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
@@ -486,8 +496,9 @@ void int8_bwd_kernel(
     }
   } else {
     for (int t = 0; t < nt; ++t) {
-      // tile t landed (t+1, t+2 may be in flight); the slot of tile t-1 is free
-      ring_wait_barrier<(G::NSLOT - 2) * G::IPW>();
+      // tile t landed (t+1, t+2 may be in flight); the slot of tile t-1 is free.  With the stagger
+      // the other half of the workgroup reads tile t+1 after this barrier: wait for it too.
+      ring_wait_barrier<(G::NSLOT - (QA_DKV_STAGGER ? 3 : 2)) * G::IPW>();
       dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
                 min(t + G::NSLOT - 1, nt - 1), lane);
       if (active) {
