@@ -162,6 +162,39 @@ def mxfp4_fwd_times(q, k, v, n):
             "frac_of_fp4_peak": flop / (tk * 1e-3) / PEAK_FP4}
 
 
+def other_configs(n):
+    """BASELINE.json's other GPU configs, each timed alone on this rank (HIP events, ms per call):
+    config 2, bf16 fwd+bwd (4,32,2048,128); config 5, the JVP forward (2,16,2048,128) with bf16
+    inputs and randn tangents.  (Config 3 is the int8 forward reported as ``int8_fwd``; config 4 is
+    the multi-GPU run of this script; config 1 is the CPU path, ``cpu_baseline``.)"""
+    from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp32
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(7)
+    out = {}
+    B, H, S, D = 4, 32, 2048, 128
+    q, k = (torch.randn((B, H, S, D), device=dev, generator=g).half() for _ in range(2))
+    v = torch.randn((B, H, S, D), device=dev, generator=g).bfloat16()
+    dO = torch.randn((B, H, S, D), device=dev, generator=g)
+
+    def bf16_step():
+        O, lse = helion_atten_bf16_fwd_training(q, k, v, False)
+        helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, False, dO)
+    t = event_time(bf16_step, n)
+    tf = event_time(lambda: helion_atten_bf16_fwd_training(q, k, v, False), n)
+    flop = 14.0 * B * H * S * S * D
+    out["cfg2_bf16_fwd_bwd"] = {"shape": [B, H, S, D], "ms": t, "TFLOPs": flop / (t * 1e-3) / 1e12,
+                                "frac_of_bf16_peak": flop / (t * 1e-3) / PEAK_BF16,
+                                "fwd_ms": tf, "fwd_TFLOPs": 4 * B * H * S * S * D / (tf * 1e-3) / 1e12}
+    del q, k, v, dO
+    B, H, S, D = 2, 16, 2048, 128
+    x = [torch.randn((B, H, S, D), device=dev, generator=g).bfloat16() for _ in range(6)]
+    t = event_time(lambda: helion_attention_jvp_forward_fp32(*x), n)
+    flop = 12.0 * B * H * S * S * D
+    out["cfg5_jvp_fwd"] = {"shape": [B, H, S, D], "ms": t, "TFLOPs": flop / (t * 1e-3) / 1e12,
+                           "frac_of_bf16_peak": flop / (t * 1e-3) / PEAK_BF16}
+    return out
+
+
 def cpu_baseline(S, D, seconds):
     """The reference's eager fp32 path (baseline_pytorch_attention fwd + autograd bwd, restated in
     oracle/restate.py) on the host cores, one (S, D) head at a time until `seconds` elapse."""
@@ -189,10 +222,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local)          # before the process group: RCCL binds this device
     dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
     B, H, S, D = (int(x) for x in a.shape.split(","))
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     q, k, v = (torch.randn((B, H, S, D), device=dev, generator=g).half() for _ in range(3))
@@ -274,6 +307,7 @@ def main():
                      "frac_of_int8_peak": 4.0 * B * H * S * S * D / (fwd_ms * 1e-3) / PEAK_I8},
         "kernel_ms": kt,
         "mxfp4_fwd": mxfp4_fwd_times(q, k, v, max(3, a.steps // 2)) if D == 128 else None,
+        "configs": None if a.skip_bf16 else other_configs(max(3, a.steps // 2)),
         "roofline": {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": PEAK_I8 / 1e12,
                      "unit": "TFLOP/s", "frac": achieved * 1e12 / PEAK_I8, "traffic": None},
     }
