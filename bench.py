@@ -109,6 +109,7 @@ def int8_kernel_times(q, k, v, dO, n):
     LD = e(N, 2, dt=torch.float32)
     qb, kb, ob = (e(N, D, dt=torch.bfloat16) for _ in range(3))
     dq, dk, dv = (e(B, H, S, D, dt=torch.float16) for _ in range(3))
+    ws = e(_lib.load().qattn_int8_bwd_ws_bytes(B * H, S, S), dt=torch.uint8)
     qks, sms = _f32(1 / math.sqrt(D) * 1.44269504), _f32(1 / math.sqrt(D))
     calls = {
         "kmean_kernel": lambda: _lib.call("qattn_kmean", P(k), P(km), B * H, S, D, st),
@@ -135,6 +136,12 @@ def int8_kernel_times(q, k, v, dO, n):
         "int8_bwd_dq_kernel": lambda: _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq),
                                                 P(ki), P(sk), P(vi), P(sv), P(LD), P(kb), P(dq),
                                                 B * H, S, D, qks, sms, st),
+        # the step's backward (qattn_int8_attn_bwd_ws): dK+dV writing the dS workspace, dQ from it
+        "int8_bwd_dkdv_kernel<dK+dV, dS out>": lambda: _lib.call(
+            "qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
+            P(qb), P(ob), P(dk), P(dv), P(ws), B * H, S, D, qks, sms, st),
+        "int8_bwd_dqw_kernel": lambda: _lib.call("qattn_int8_bwd_dq_ws", P(kb), P(sk), P(dq), P(ws),
+                                                 B * H, S, D, sms, st),
     }
     order = list(calls)
     for name in order:  # populate every buffer once in dependency order
@@ -276,10 +283,10 @@ def main():
             dist.destroy_process_group()
         return
     kt = int8_kernel_times(q, k, v, dO, max(3, a.steps // 2))
-    per_call = {  # algorithmic MFMA work per launch
+    per_call = {  # algorithmic MFMA work per launch, the step's kernels
         "int8_attn_fwd_kernel": 4.0 * B * H * S * S * D,   # QK^T, PV
-        "int8_bwd_dkdv_kernel<dK+dV>": 8.0 * B * H * S * S * D,   # S, dP, dV, dK (the step's kernel)
-        "int8_bwd_dq_kernel": 6.0 * B * H * S * S * D,     # S, dP (recomputed), dQ
+        "int8_bwd_dkdv_kernel<dK+dV, dS out>": 8.0 * B * H * S * S * D,   # S, dP, dV, dK
+        "int8_bwd_dqw_kernel": 2.0 * B * H * S * S * D,    # dQ (S, dP, dS come from the workspace)
     }
     dom = max(per_call, key=lambda n: kt[n])
     achieved = per_call[dom] / (kt[dom] * 1e-3) / 1e12

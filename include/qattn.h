@@ -103,6 +103,29 @@ int qattn_int8_attn_bwd_ex(const void* dO_i8, const void* sdO, const void* q_i8,
                            void* dq, void* dk, void* dv, long bh, long sq_tok, long sk_tok, int group,
                            int causal, int head_dim, float qks, float sms, void* stream);
 
+/* qattn_int8_attn_bwd_ex with a caller-provided dS workspace (no recomputation in the dQ pass):
+ * the fused dK+dV kernel also stores each quantised 32x32 dS tile (dS_i8, 1 KiB, and its scale
+ * s_dS) in ws, and the dQ kernel reads them back instead of recomputing S, dP, P and dS
+ * (attention_int8.py:399-420).  dq, dk, dv are bit-identical to qattn_int8_attn_bwd_ex's.
+ * ws must hold qattn_int8_bwd_ws_bytes(bh, sq_tok, sk_tok) bytes, 16-byte aligned; it is scratch
+ * (overwritten, not read before written).  Returns 1 for ws == NULL. */
+long qattn_int8_bwd_ws_bytes(long bh, long sq_tok, long sk_tok);
+int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                           const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                           const void* LD, const void* q_bf, const void* k_bf, const void* dO_bf,
+                           void* dq, void* dk, void* dv, void* ws, long bh, long sq_tok, long sk_tok,
+                           int group, int causal, int head_dim, float qks, float sms, void* stream);
+
+/* The two parts of qattn_int8_attn_bwd_ws (square, ungrouped, non-causal), launchable alone:
+ * dK + dV writing the dS workspace, then dQ reading it. */
+int qattn_int8_bwd_dkdv_ws(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                           const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                           const void* LD, const void* q_bf, const void* dO_bf, void* dk, void* dv,
+                           void* ws, long bh, long seq, int head_dim, float qks, float sms,
+                           void* stream);
+int qattn_int8_bwd_dq_ws(const void* k_bf, const void* sk, void* dq, void* ws, long bh, long seq,
+                         int head_dim, float sms, void* stream);
+
 /* The parts of qattn_int8_attn_bwd, launchable alone (per-kernel timing / overlap):
  * dK and dV (attention_int8.py:375-378, 423-428), dV only, dK only, dQ only (414-420). */
 int qattn_int8_bwd_dkdv(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,

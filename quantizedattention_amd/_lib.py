@@ -30,6 +30,11 @@ SIGNATURES = {
     "qattn_int8_attn_fwd_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
     "qattn_int8_attn_bwd_ex": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                              _c_float, _vp],
+    "qattn_int8_attn_bwd_ws": [_vp] * 16 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
+                                             _c_float, _vp],
+    "qattn_int8_bwd_ws_bytes": [_c_long, _c_long, _c_long],
+    "qattn_int8_bwd_dkdv_ws": [_vp] * 14 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
+    "qattn_int8_bwd_dq_ws": [_vp] * 4 + [_c_long, _c_long, _c_int, _c_float, _vp],
     "qattn_int8_bwd_prep": [_vp] * 7 + [_c_long, _c_long, _c_int, _vp],
     "qattn_i8_to_bf16": [_vp, _vp, _c_long, _vp],
     "qattn_int8_attn_bwd": [_vp] * 15 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
@@ -60,6 +65,9 @@ SIGNATURES = {
     "qattn_probe_fwd_helpers": [_vp] * 7,
 }
 
+# return types other than the int status code
+RESTYPES = {"qattn_int8_bwd_ws_bytes": ctypes.c_long}
+
 _lib = None
 
 
@@ -83,7 +91,7 @@ def load(path: os.PathLike | None = None) -> ctypes.CDLL:
         if fn is None:
             raise QAttnError(f"{p} does not export {name} (stale build? rebuild it)")
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_int
+        fn.restype = RESTYPES.get(name, ctypes.c_int)
     _lib = lib
     return lib
 

@@ -20,6 +20,7 @@ the reference-shaped one.
 from __future__ import annotations
 
 import math
+import os
 from typing import Tuple
 
 import torch
@@ -106,11 +107,18 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     return O, lse, q_i8, k_i8.t(), v_i8, sq, sk, sv, k_mean, q_bf, k_bf
 
 
+# Largest dS workspace (bytes) the backward allocates to skip the dQ pass's recomputation of S,
+# dP, P and dS (qattn_int8_attn_bwd_ws); larger problems recompute (qattn_int8_attn_bwd_ex).  The
+# results are bit-identical either way.  1 B per score + 4 B per 32x32 tile: 2.2 GB at (4,32,4096).
+WS_MAX_BYTES = int(os.environ.get("QATTN_BWD_WS_MAX", 16 << 30))
+
+
 def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=None, causal=False,
-                   kv_heads=None):
+                   kv_heads=None, use_ws=None):
     """Corrected int8 backward; q_bf / k_bf: bf16 images from the forward (computed here if None).
 
-    kv_heads: key/value heads (default: those of O); their token count follows from k_i8T."""
+    kv_heads: key/value heads (default: those of O); their token count follows from k_i8T.
+    use_ws: dQ from the dS workspace (True), by recomputation (False), or by size (None)."""
     O = O.to(torch.float16).contiguous()
     dO = dO.to(torch.float16).contiguous()
     _lib.require_gpu(dO, O, q_i8)
@@ -145,11 +153,18 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
     dv = torch.empty((B, Hkv, Sk, D), dtype=torch.float16, device=dev)
     qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
     sms = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
-    _lib.call("qattn_int8_attn_bwd_ex", _lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8),
-              _lib.ptr(sq.contiguous()), _lib.ptr(k_i8), _lib.ptr(sk.contiguous()),
-              _lib.ptr(v_i8), _lib.ptr(sv.contiguous()), _lib.ptr(LD), _lib.ptr(q_bf),
-              _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
-              B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms, st)
+    common = (_lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8), _lib.ptr(sq.contiguous()), _lib.ptr(k_i8),
+              _lib.ptr(sk.contiguous()), _lib.ptr(v_i8), _lib.ptr(sv.contiguous()), _lib.ptr(LD),
+              _lib.ptr(q_bf), _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv))
+    shape = (B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms, st)
+    ws_bytes = _lib.load().qattn_int8_bwd_ws_bytes(B * H, S, Sk)
+    if use_ws is None:
+        use_ws = 0 <= ws_bytes <= WS_MAX_BYTES
+    if use_ws and ws_bytes > 0:
+        ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
+        _lib.call("qattn_int8_attn_bwd_ws", *common, _lib.ptr(ws), *shape)
+    else:
+        _lib.call("qattn_int8_attn_bwd_ex", *common, *shape)
     return dq, dk, dv
 
 

@@ -263,7 +263,11 @@ QA_DEVICE float max16_abs3(const float* x) {
 // starting at row (bh / ydiv) * Ny of the streamed tensors -- dK/dV: the G query heads that share a
 // key/value head (Ny = G * Sq, contiguous), dQ: the key/value head of the query head (ydiv = G,
 // Ny = Sk).  CAUSAL drops key > query (positions: streamed row mod Smod).
-template <int D, int ROLE, bool CAUSAL = false>
+// WS (ROLE_DKV only): also write every quantised dS tile (dS_i8 in this kernel's register order,
+// 16 bytes per lane, and its scale s_dS) to the dS workspace that int8_bwd_dqw_kernel reads, so the
+// dQ pass does not recompute S, dP, P and dS.  Tile record (query head, q-tile, key tile) =
+// ((bh_q * nqt + qt) * nkt + kt): 1024 bytes in ds8, one float in sds.
+template <int D, int ROLE, bool CAUSAL = false, bool WS = false>
 __global__ __launch_bounds__((64 * BwdCfg<D, ROLE>::WAVES), (8 / BwdCfg<D, ROLE>::WAVES))
 void int8_bwd_kernel(
     const int8_t* __restrict__ x8a, const int8_t* __restrict__ x8b, const _Float16* __restrict__ sxa,
@@ -271,10 +275,12 @@ void int8_bwd_kernel(
     const __bf16* __restrict__ ytr, const __bf16* __restrict__ ytr2, const float2* __restrict__ yld,
     const _Float16* __restrict__ sya, const _Float16* __restrict__ syb,
     const float2* __restrict__ xld, _Float16* __restrict__ out, _Float16* __restrict__ out2, int BH,
-    int Sx, int Ny, int ydiv, int Smod, float qks, float sms) {
+    int Sx, int Ny, int ydiv, int Smod, float qks, float sms, int8_t* __restrict__ ds8,
+    float* __restrict__ sds) {
   using C = I8BwdCfg<D>;
   using G = BwdCfg<D, ROLE>;
   constexpr bool TWO = G::TWO;
+  static_assert(!WS || ROLE == ROLE_DKV, "the dS workspace is written by the fused dK+dV kernel");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
   int bh, xt;
@@ -347,11 +353,8 @@ void int8_bwd_kernel(
   // int8 products of tile t: S (and dP)
   auto products = [&](int t, v16i& sa, v16i& pa) {
     const char* base = slot(t);
-    // DQ: accumulators start at the bit pattern of 1.5*2^23, so the int32 result read as fp32 is
-    // exactly 1.5*2^23 + acc (|acc| < 2^22): no int->float conversion per score (see values())
-    constexpr int bias = (ROLE == ROLE_DQ) ? 0x4B400000 : 0;
-    sa = v16i{} + bias;
-    pa = v16i{} + bias;
+    sa = v16i{};
+    pa = v16i{};
 #pragma unroll
     for (int s = 0; s < C::NKS8; ++s) {
       sa = mfma_i8(*reinterpret_cast<const v4i*>(base + G::Y8A + roff[s]), xa[s], sa);
@@ -392,15 +395,13 @@ void int8_bwd_kernel(
         }
       }
     } else {
-      // per-lane row stats: fold the 1.5*2^23 accumulator bias into the constants (one rounding of
-      // the constant, well below the int8 quantisation noise)
-      constexpr float M = 12582912.0f;
-      const float k1 = -fmaf(c1, M, lsex), k2 = -fmaf(c2, M, Dx);
+      // per-lane row stats; the same operations as the dK/dV kernels' (so every kernel quantises a
+      // dS tile to the same dS_i8 and scale, and the dS workspace path is bit-identical to this one)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p = exp2_f32(fmaf(__int_as_float(sa[i]), c1, k1));
+        float p = exp2_f32(fmaf((float)sa[i], c1, -lsex));
         if (diag && y0 + (i & 3) + 8 * (i >> 2) + 4 * h > x0 + c32) p = 0.f;   // key > query
-        dS[i] = p * fmaf(__int_as_float(pa[i]), c2, k2);
+        dS[i] = p * fmaf((float)pa[i], c2, -Dx);
       }
     }
   };
@@ -432,6 +433,57 @@ void int8_bwd_kernel(
   // DK/DKV-dS: q of the q tile (sya); DQ: k of the k tile (sya)
   auto so_p = [&](int t) { return (float)sc_lds[nt + t]; };
   auto so_ds = [&](int t) { return (float)sc_lds[t]; };
+  // dS workspace of this key/value head's G query heads: records (bh*G*nqt + t) * nkt + kt for the
+  // streamed tile t (= g * nqt + qt) -- one contiguous region per key/value head (< 4 GiB)
+  const long ws_first = WS ? (long)bh * (Ny / 32) * (Sx / 32) : 0;
+  const int ws_nrec = WS ? (Ny / 32) * (Sx / 32) : 0;
+  const __amdgpu_buffer_rsrc_t ws_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(ds8 + ws_first * 1024, 0, ws_nrec * 1024, 0x00020000);
+  // the tile scales s_dS stay in LDS until the loop ends (one VMEM store per tile, not two)
+  float* sds_lds = reinterpret_cast<float*>(smem + G::NSLOT * G::SLOT +
+                                            ((2 * nt * 2 + 15) / 16) * 16);
+  // dS quantisation (the dK operand, as quantise()) that also emits the workspace record of tile t:
+  // the 16 dS_i8 of this lane packed in index order, and s_dS (lane 0).  Two VMEM stores per tile,
+  // counted by the ring waits below (WS_OPS).
+  auto quantise_ds = [&](const float* X, int t, v8bf* op) {
+    if constexpr (!WS) {
+      quantise(X, so_ds(t), op);
+    } else {
+      const float xmax = wave_max_dpp(max16_abs3(X));
+      const float sx = xmax * (1.0f / 127.0f);
+      const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
+      const float c = sx * so_ds(t);
+      float q[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) q[i] = __builtin_truncf(X[i] * inv);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        v4u w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = pk_bf16(q[8 * s + 2 * j] * c, q[8 * s + 2 * j + 1] * c);
+        op[s] = __builtin_bit_cast(v8bf, w);
+      }
+      v4i bytes;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const unsigned lo = __builtin_amdgcn_perm((unsigned)(int)q[4 * d + 1], (unsigned)(int)q[4 * d],
+                                                  0x0c0c0400u);
+        const unsigned hi = __builtin_amdgcn_perm((unsigned)(int)q[4 * d + 3], (unsigned)(int)q[4 * d + 2],
+                                                  0x0c0c0400u);
+        bytes[d] = (int)__builtin_amdgcn_perm(hi, lo, 0x05040100u);
+      }
+      // record of (query head bh*G + t/nqt, q-tile t%nqt, key tile x0/32), relative to this key/value
+      // head's first record (ws_rsrc / sc_rsrc): SGPR offsets, no per-lane address arithmetic
+      const int nqt = Smod / 32, nkt = Sx / 32;
+      const unsigned rel = (unsigned)(t * nkt + x0 / 32);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, bytes), ws_rsrc, 16 * lane,
+                                             (int)(rel * 1024u), 0);
+      (void)nqt;
+      if (lane == 0) sds_lds[wave * nt + t] = sx;   // written out after the loop
+    }
+  };
+  // VMEM operations per tile besides the ring DMA (the workspace store of an active wave)
+  constexpr int WS_OPS = WS ? 1 : 0;
 
   vmem_drain();
   __syncthreads();
@@ -469,14 +521,17 @@ void int8_bwd_kernel(
       products(0, sa, pa);
       float P[16], dS[16];
       values(0, sa, pa, P, dS);
-      quantise(dS, so_ds(0), opS);
+      quantise_ds(dS, 0, opS);
       quantise(P, so_p(0), opP);
     }
 #if QA_DKV_PRIO
     __builtin_amdgcn_s_setprio(1);
 #endif
     for (int t = 0; t < nt; ++t) {
-      ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
+      // tile t+1 landed: younger than its DMA are the workspace stores of tile t-1, the DMA of
+      // tile t+2 and the stores of tile t
+      if (active) ring_wait_barrier<(G::NSLOT - 3) * G::IPW + 2 * WS_OPS>();
+      else ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
       dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
                 min(t + G::NSLOT - 1, nt - 1), lane);
       if (active) {
@@ -490,7 +545,7 @@ void int8_bwd_kernel(
         accumulate(acc2, ta, opP);         // dV += dO^T P
         float P[16], dS[16];
         values(tn, sa, pa, P, dS);
-        quantise(dS, so_ds(tn), opS);
+        quantise_ds(dS, tn, opS);
         quantise(P, so_p(tn), opP);
       }
     }
@@ -498,7 +553,12 @@ void int8_bwd_kernel(
     for (int t = 0; t < nt; ++t) {
       // tile t landed (t+1, t+2 may be in flight); the slot of tile t-1 is free.  With the stagger
       // the other half of the workgroup reads tile t+1 after this barrier: wait for it too.
-      ring_wait_barrier<(G::NSLOT - (QA_DKV_STAGGER ? 3 : 2)) * G::IPW>();
+      // (the workspace stores of an active wave, WS_OPS per tile, sit between the DMAs)
+      if (active)
+        ring_wait_barrier<(G::NSLOT - (QA_DKV_STAGGER ? 3 : 2)) * G::IPW +
+                          (QA_DKV_STAGGER ? 2 : 3) * WS_OPS>();
+      else
+        ring_wait_barrier<(G::NSLOT - (QA_DKV_STAGGER ? 3 : 2)) * G::IPW>();
       dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
                 min(t + G::NSLOT - 1, nt - 1), lane);
       if (active) {
@@ -507,7 +567,7 @@ void int8_bwd_kernel(
         float P[16], dS[16];
         values(t, sa, pa, P, dS);
         v8bf opS[2], opP[2];
-        quantise(dS, so_ds(t), opS);
+        quantise_ds(dS, t, opS);
         quantise(P, so_p(t), opP);
         v8bf ta[2 * C::NDB];
         tr_load(t, G::TR, ta);
@@ -519,6 +579,10 @@ void int8_bwd_kernel(
   }
   vmcnt_wait_all();
   if (!active) return;
+  if constexpr (WS) {   // this wave's s_dS column: record (t, x0/32) of the key/value head
+    const int nkt = Sx / 32;
+    for (int t = lane; t < nt; t += 64) sds[ws_first + (long)t * nkt + x0 / 32] = sds_lds[wave * nt + t];
+  }
   const long r = hrow + x0 + c32;
   auto store = [&](const v16f* ac, float osc, _Float16* dst) {
 #pragma unroll
@@ -534,6 +598,165 @@ void int8_bwd_kernel(
   };
   store(acc, ROLE == ROLE_DV ? 1.0f : sms, out);
   if constexpr (ROLE == ROLE_DKV) store(acc2, 1.0f, out2);
+}
+
+
+// ------------------------------------------------------------- dQ from the dS workspace (WS)
+// The fused dK+dV kernel (WS) leaves every quantised dS tile in the workspace: dS_i8 in its own
+// register order (key on the lane: lane l holds key l%32 and the 16 queries 8(i/4) + 4(l/32) + i%4,
+// byte i) and the tile scale s_dS.  Here a wave owns 32 queries and streams 32-key tiles: the k
+// image through the LDS ring as in int8_bwd_kernel<ROLE_DQ>, its own 1 KiB dS record of the tile
+// beside it.  One v_mfma_i32_32x32x32_i8 against a permutation matrix P brings the record into the
+// dQ order (query on the lane, keys 8(i/4) + 4(l/32) + i%4: C = A P with A = the record, rows =
+// keys), and the tile then takes exactly the operand / MFMA sequence of the ROLE_DQ kernel:
+// op = bf16(dS_i8 * (s_dS * sk)), dQ^T += K^T op.  The result is bit-identical to that kernel's,
+// which recomputes S, dP, P and dS (2 int8 MFMA chains, ~150 VALU per tile) where this pass spends
+// one int8 MFMA and ~40 VALU.
+#ifndef QA_DQW_WAVES
+#define QA_DQW_WAVES 8
+#endif
+template <int D>
+struct DqwCfg {
+  static constexpr int WAVES = QA_DQW_WAVES;
+  static constexpr int T16 = 64 * D;               // bf16 k image of a 32-key tile (L2-resident)
+  static constexpr int NSLOT = 4;                  // k image ring: 3 tiles ahead
+  static constexpr int RSLOT = WAVES == 8 ? 5 : 10;   // record ring (HBM stream)
+  static constexpr int REC = WAVES * 1024;         // the waves' dS records of one tile
+  static constexpr int RBASE = NSLOT * T16;
+  static constexpr int NP16 = T16 / 1024;
+  // k image pieces per wave per tile; with more waves than pieces the extra waves re-issue a
+  // piece (the same bytes to the same place), so every wave issues IPK + 1 DMAs per tile
+  static constexpr int IPK = (NP16 + WAVES - 1) / WAVES;
+};
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(64 * QA_DQW_WAVES, 2) void int8_bwd_dqw_kernel(
+    const int8_t* __restrict__ ds8, const float* __restrict__ sds, const __bf16* __restrict__ kbf,
+    const _Float16* __restrict__ sk, _Float16* __restrict__ dq, int BH, int Sq, int Sk, int G,
+    float sms) {
+  using C = I8BwdCfg<D>;
+  using W = DqwCfg<D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nqb = (Sq + 32 * W::WAVES - 1) / (32 * W::WAVES);
+  int bh, qb;
+  xcd_remap(blockIdx.x, nqb, BH, bh, qb);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int q0 = qb * 32 * W::WAVES + wave * 32;
+  const bool active = q0 < Sq;
+  const int nqt = Sq / 32, nkt = Sk / 32;
+  const long kv_row0 = (long)(bh / G) * Sk;
+  // causal: key tiles past the workgroup's last query are all zero for its rows (as ROLE_DQ)
+  const int nt = CAUSAL ? min(nkt, (qb * 32 * W::WAVES + 32 * W::WAVES) / 32) : nkt;
+  const long rec0 = ((long)bh * nqt + (active ? q0 / 32 : 0)) * nkt;   // this wave's first record
+
+  // DMA plan: pieces of the k image (swizzled rows, as BwdDma's TR region), and the own record
+  unsigned kvoff[W::IPK], klds[W::IPK];
+  v4u krsrc[W::IPK];
+#pragma unroll
+  for (int i = 0; i < W::IPK; ++i) {
+    int pc = wave + W::WAVES * i;
+    if (pc >= W::NP16) pc = wave % W::NP16;
+    constexpr int NCH = 2 * D / 16, RPI = 64 / NCH;
+    const int row = pc * RPI + lane / NCH, c = lane % NCH;
+    kvoff[i] = row * 2 * D + 16 * (c ^ t16_sw<D>(row));
+    klds[i] = pc * 1024;
+    krsrc[i] = make_rsrc(kbf + kv_row0 * D, (unsigned)Sk * 2 * D);
+  }
+  // an inactive wave's descriptor has no records: its loads return zeros, nothing is read
+  const v4u rrsrc = make_rsrc(ds8 + rec0 * 1024, active ? (unsigned)nkt * 1024u : 0u);
+  const unsigned smem_lds = lds_addr(smem);
+  auto issue_k = [&](int t) {
+    const unsigned sl = smem_lds + (t % W::NSLOT) * W::T16;
+#pragma unroll
+    for (int i = 0; i < W::IPK; ++i) dma16_buf(krsrc[i], kvoff[i], (unsigned)min(t, nt - 1) * 64u * D, sl + klds[i]);
+  };
+  auto issue_r = [&](int t) {
+    dma16_buf(rrsrc, 16u * lane, (unsigned)min(t, nt - 1) * 1024u,
+              smem_lds + W::RBASE + (t % W::RSLOT) * W::REC + wave * 1024);
+  };
+#pragma unroll
+  for (int i = 0; i < W::NSLOT - 1; ++i) issue_k(i);
+  for (int i = 0; i < W::RSLOT - 1; ++i) issue_r(i);
+  // per-tile scales: s_dS of each wave's records, sk of the key tiles (once, in LDS)
+  float* sds_lds = reinterpret_cast<float*>(smem + W::RBASE + W::RSLOT * W::REC);
+  _Float16* sk_lds = reinterpret_cast<_Float16*>(sds_lds + W::WAVES * nkt);
+  if (active)
+    for (int i = lane; i < nt; i += 64) sds_lds[wave * nkt + i] = sds[rec0 + i];
+  for (int i = tid; i < nt; i += 64 * W::WAVES) sk_lds[i] = sk[kv_row0 / 32 + i];
+
+  // permutation operand: byte i of lane l is 1 iff query 8(i/4) + 4(l/32) + i%4 is this lane's
+  // column l%32 (one byte in the lane half that holds it)
+  v4i perm = {0, 0, 0, 0};
+  if (((c32 >> 2) & 1) == h) {
+    const int i = 4 * (c32 >> 3) + (c32 & 3);
+    perm[i >> 2] = 1 << (8 * (i & 3));
+  }
+  int troff[C::NDB];
+  {
+    const int gg = (lane >> 4) & 1, i16 = lane & 15;
+    const int row = 4 * h + (i16 >> 2);
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) {
+      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
+      troff[b] = row * 2 * D + 16 * ((d / 8) ^ t16_sw<D>(row)) + (d % 8) * 2;
+    }
+  }
+  v16f acc[C::NDB];
+#pragma unroll
+  for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
+
+  vmem_drain();
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    // tile t's k image landed (its record, issued earlier, too): younger than the k DMA of tile t
+    // are the record DMA issued with it and the k + record DMAs of the two iterations since
+    ring_wait_barrier<1 + (W::NSLOT - 2) * (W::IPK + 1)>();
+    issue_k(t + W::NSLOT - 1);
+    issue_r(t + W::RSLOT - 1);
+    if (active) {
+      const char* kb = smem + (t % W::NSLOT) * W::T16;
+      const v4i rec = *reinterpret_cast<const v4i*>(smem + W::RBASE + (t % W::RSLOT) * W::REC +
+                                                    wave * 1024 + 16 * lane);
+      v8bf ta[2 * C::NDB];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int b = 0; b < C::NDB; ++b) {
+          const char* a = kb + troff[b] + 16 * s * 2 * D;
+          ta[s * C::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * 2 * D));
+        }
+      const v16i x = mfma_i8(rec, perm, v16i{});   // dS_i8 in dQ order (exact integers)
+      const float c = sds_lds[wave * nkt + t] * (float)sk_lds[t];
+      v8bf op[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        v4u w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          w[j] = pk_bf16((float)x[8 * s + 2 * j] * c, (float)x[8 * s + 2 * j + 1] * c);
+        op[s] = __builtin_bit_cast(v8bf, w);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int b = 0; b < C::NDB; ++b) acc[b] = mfma_bf16(ta[s * C::NDB + b], op[s], acc[b]);
+    }
+  }
+  vmcnt_wait_all();
+  if (!active) return;
+  const long r = (long)bh * Sq + q0 + c32;
+#pragma unroll
+  for (int b = 0; b < C::NDB; ++b) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      v4h w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * sms);
+      *reinterpret_cast<v4h*>(dq + r * D + 32 * b + 8 * g + 4 * h) = w;
+    }
+  }
 }
 
 }  // namespace qattn
@@ -571,47 +794,74 @@ extern "C" int qattn_i8_to_bf16(const void* x, void* y, long n, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-template <int D, int ROLE, bool CAUSAL>
+template <int D, int ROLE, bool CAUSAL, bool WS>
 static void launch_bwd_c(const void* x8a, const void* x8b, const void* sxa, const void* sxb,
                          const void* y8a, const void* y8b, const void* ytr, const void* ytr2,
                          const void* yld, const void* sya, const void* syb, const void* xld, void* out,
                          void* out2, long bhx, long sx, long ny, int ydiv, long smod, float qks,
-                         float sms, hipStream_t st) {
+                         float sms, void* ds8, void* sds, hipStream_t st) {
   using G = BwdCfg<D, ROLE>;
-  const int lds = G::NSLOT * G::SLOT + (int)((2 * (ny / 32) * 2 + 15) / 16 * 16);
-  hipFuncSetAttribute((const void*)int8_bwd_kernel<D, ROLE, CAUSAL>,
+  const int lds = G::NSLOT * G::SLOT + (int)((2 * (ny / 32) * 2 + 15) / 16 * 16) +
+                  (WS ? G::WAVES * (int)(ny / 32) * 4 : 0);
+  hipFuncSetAttribute((const void*)int8_bwd_kernel<D, ROLE, CAUSAL, WS>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
-  hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE, CAUSAL>), dim3((unsigned)(nb * bhx)),
+  hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE, CAUSAL, WS>), dim3((unsigned)(nb * bhx)),
                      dim3(64 * G::WAVES), lds, st, (const int8_t*)x8a, (const int8_t*)x8b,
                      (const _Float16*)sxa, (const _Float16*)sxb, (const int8_t*)y8a,
                      (const int8_t*)y8b, (const __bf16*)ytr, (const __bf16*)ytr2, (const float2*)yld,
                      (const _Float16*)sya, (const _Float16*)syb, (const float2*)xld, (_Float16*)out,
-                     (_Float16*)out2, (int)bhx, (int)sx, (int)ny, ydiv, (int)smod, qks, sms);
+                     (_Float16*)out2, (int)bhx, (int)sx, (int)ny, ydiv, (int)smod, qks, sms,
+                     (int8_t*)ds8, (float*)sds);
 }
-template <int D, int ROLE>
+template <int D, int ROLE, bool WS = false>
 static void launch_bwd(int causal, const void* x8a, const void* x8b, const void* sxa, const void* sxb,
                        const void* y8a, const void* y8b, const void* ytr, const void* ytr2,
                        const void* yld, const void* sya, const void* syb, const void* xld, void* out,
                        void* out2, long bhx, long sx, long ny, int ydiv, long smod, float qks,
-                       float sms, hipStream_t st) {
+                       float sms, hipStream_t st, void* ds8 = nullptr, void* sds = nullptr) {
   if (causal)
-    launch_bwd_c<D, ROLE, true>(x8a, x8b, sxa, sxb, y8a, y8b, ytr, ytr2, yld, sya, syb, xld, out, out2,
-                                bhx, sx, ny, ydiv, smod, qks, sms, st);
+    launch_bwd_c<D, ROLE, true, WS>(x8a, x8b, sxa, sxb, y8a, y8b, ytr, ytr2, yld, sya, syb, xld, out,
+                                    out2, bhx, sx, ny, ydiv, smod, qks, sms, ds8, sds, st);
   else
-    launch_bwd_c<D, ROLE, false>(x8a, x8b, sxa, sxb, y8a, y8b, ytr, ytr2, yld, sya, syb, xld, out, out2,
-                                 bhx, sx, ny, ydiv, smod, qks, sms, st);
+    launch_bwd_c<D, ROLE, false, WS>(x8a, x8b, sxa, sxb, y8a, y8b, ytr, ytr2, yld, sya, syb, xld, out,
+                                     out2, bhx, sx, ny, ydiv, smod, qks, sms, ds8, sds, st);
 }
 
-// which: bit mask 1 = dV kernel, 4 = dK kernel, 8 = fused dK+dV kernel, 2 = dQ kernel.
+template <int D, bool CAUSAL>
+static void launch_dqw_c(const void* ds8, const void* sds, const void* k_bf, const void* sk, void* dq,
+                         long bh, long sqt, long skt, int group, float sms, hipStream_t st) {
+  using G = DqwCfg<D>;
+  const int nkt = (int)(skt / 32);
+  const int lds = G::RBASE + G::RSLOT * G::REC + G::WAVES * nkt * 4 + (nkt * 2 + 15) / 16 * 16;
+  hipFuncSetAttribute((const void*)int8_bwd_dqw_kernel<D, CAUSAL>,
+                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  const int nb = (int)((sqt + 32 * G::WAVES - 1) / (32 * G::WAVES));
+  hipLaunchKernelGGL((int8_bwd_dqw_kernel<D, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
+                     lds, st, (const int8_t*)ds8, (const float*)sds, (const __bf16*)k_bf,
+                     (const _Float16*)sk, (_Float16*)dq, (int)bh, (int)sqt, (int)skt, group, sms);
+}
+
+// which: bit mask 1 = dV kernel, 4 = dK kernel, 8 = fused dK+dV kernel, 2 = dQ kernel,
+// 16 = fused dK+dV kernel writing the dS workspace ws, 32 = dQ from the dS workspace.
 // bh = batch * query heads; the key/value side has bh / group heads of skt rows.
 template <int D>
 static void bwd_launch_d(int which, const void* dO_i8, const void* sdO, const void* q_i8,
                          const void* sq, const void* k_i8, const void* sk, const void* v_i8,
                          const void* sv, const void* LD, const void* q_bf, const void* k_bf,
                          const void* dO_bf, void* dq, void* dk, void* dv, long bh, long sqt, long skt,
-                         int group, int causal, float qks, float sms, hipStream_t st) {
+                         int group, int causal, float qks, float sms, hipStream_t st,
+                         void* ws = nullptr) {
   const long bkv = bh / group, ny = group * sqt;
+  char* ds8 = (char*)ws;
+  char* sds = ws ? ds8 + bh * (sqt / 32) * (skt / 32) * 1024 : nullptr;
+  if (which & 16)
+    launch_bwd<D, ROLE_DKV, true>(causal, k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, dO_bf, LD, sq, sdO,
+                                  nullptr, dk, dv, bkv, skt, ny, 1, sqt, qks, sms, st, ds8, sds);
+  if (which & 32) {
+    if (causal) launch_dqw_c<D, true>(ds8, sds, k_bf, sk, dq, bh, sqt, skt, group, sms, st);
+    else launch_dqw_c<D, false>(ds8, sds, k_bf, sk, dq, bh, sqt, skt, group, sms, st);
+  }
   // dV: own K (x8a) / streamed Q8 (y8a), dO image (ytr), LD; scales: sk|sv own, sq|sdO streamed
   if (which & 1)
     launch_bwd<D, ROLE_DV>(causal, k_i8, nullptr, sk, sv, q_i8, nullptr, dO_bf, nullptr, LD, sq, sdO,
@@ -635,7 +885,7 @@ static int int8_bwd_launch(int which, const void* dO_i8, const void* sdO, const 
                            const void* sv, const void* LD, const void* q_bf, const void* k_bf,
                            const void* dO_bf, void* dq, void* dk, void* dv, long bh, long sqt,
                            long skt, int group, int causal, int head_dim, float qks, float sms,
-                           void* stream) {
+                           void* stream, void* ws = nullptr) {
   if (sqt % 32 != 0 || skt % 32 != 0 || group < 1 || bh % group != 0 ||
       (head_dim != 64 && head_dim != 128))
     return 1;
@@ -643,10 +893,10 @@ static int int8_bwd_launch(int which, const void* dO_i8, const void* sdO, const 
   hipStream_t st = (hipStream_t)stream;
   if (head_dim == 128)
     bwd_launch_d<128>(which, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
-                      dv, bh, sqt, skt, group, causal, qks, sms, st);
+                      dv, bh, sqt, skt, group, causal, qks, sms, st, ws);
   else
     bwd_launch_d<64>(which, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq, dk,
-                     dv, bh, sqt, skt, group, causal, qks, sms, st);
+                     dv, bh, sqt, skt, group, causal, qks, sms, st, ws);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -698,4 +948,40 @@ extern "C" int qattn_int8_bwd_dq(const void* dO_i8, const void* sdO, const void*
                                  long seq, int head_dim, float qks, float sms, void* stream) {
   return int8_bwd_launch(2, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, nullptr, k_bf, nullptr, dq,
                          nullptr, nullptr, bh, seq, seq, 1, 0, head_dim, qks, sms, stream);
+}
+
+extern "C" long qattn_int8_bwd_ws_bytes(long bh, long sq_tok, long sk_tok) {
+  if (sq_tok % 32 != 0 || sk_tok % 32 != 0 || bh < 0) return -1;
+  return bh * (sq_tok / 32) * (sk_tok / 32) * (1024 + 4);
+}
+
+extern "C" int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const void* q_i8,
+                                      const void* sq, const void* k_i8, const void* sk,
+                                      const void* v_i8, const void* sv, const void* LD,
+                                      const void* q_bf, const void* k_bf, const void* dO_bf, void* dq,
+                                      void* dk, void* dv, void* ws, long bh, long sq_tok, long sk_tok,
+                                      int group, int causal, int head_dim, float qks, float sms,
+                                      void* stream) {
+  if (ws == nullptr) return 1;
+  return int8_bwd_launch(16 | 32, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq,
+                         dk, dv, bh, sq_tok, sk_tok, group, causal, head_dim, qks, sms, stream, ws);
+}
+
+// The two parts of qattn_int8_attn_bwd_ws, launchable alone (per-kernel timing).
+extern "C" int qattn_int8_bwd_dkdv_ws(const void* dO_i8, const void* sdO, const void* q_i8,
+                                      const void* sq, const void* k_i8, const void* sk,
+                                      const void* v_i8, const void* sv, const void* LD,
+                                      const void* q_bf, const void* dO_bf, void* dk, void* dv, void* ws,
+                                      long bh, long seq, int head_dim, float qks, float sms,
+                                      void* stream) {
+  if (ws == nullptr) return 1;
+  return int8_bwd_launch(16, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, nullptr, dO_bf,
+                         nullptr, dk, dv, bh, seq, seq, 1, 0, head_dim, qks, sms, stream, ws);
+}
+extern "C" int qattn_int8_bwd_dq_ws(const void* k_bf, const void* sk, void* dq, void* ws, long bh,
+                                    long seq, int head_dim, float sms, void* stream) {
+  if (ws == nullptr) return 1;
+  return int8_bwd_launch(32, nullptr, nullptr, nullptr, nullptr, nullptr, sk, nullptr, nullptr,
+                         nullptr, nullptr, k_bf, nullptr, dq, nullptr, nullptr, bh, seq, seq, 1, 0,
+                         head_dim, 0.f, sms, stream, ws);
 }

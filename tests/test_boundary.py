@@ -23,10 +23,16 @@ def header_decls():
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
-    for m in re.finditer(r"\bint\s+(qattn_\w+)\s*\(([^)]*)\)\s*;", text):
-        params = [p.strip() for p in m.group(2).split(",") if p.strip()]
-        decls[m.group(1)] = params
+    for m in re.finditer(r"\b(int|long)\s+(qattn_\w+)\s*\(([^)]*)\)\s*;", text):
+        params = [p.strip() for p in m.group(3).split(",") if p.strip()]
+        decls[m.group(2)] = params
     return decls
+
+
+def header_returns():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return {m.group(2): m.group(1)
+            for m in re.finditer(r"\b(int|long)\s+(qattn_\w+)\s*\(([^)]*)\)\s*;", text)}
 
 
 def test_header_parses():
@@ -68,8 +74,8 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_and_types():
     from quantizedattention_amd import _lib
     lib = _lib.load()
-    for name in header_decls():
-        assert getattr(lib, name).restype is ctypes.c_int
+    for name, ret in header_returns().items():
+        assert getattr(lib, name).restype is (ctypes.c_long if ret == "long" else ctypes.c_int), name
 
 
 def test_int8_error_messages():

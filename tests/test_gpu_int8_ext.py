@@ -108,3 +108,23 @@ def test_int8_autograd_gqa_causal(lib):
                             causal=True)
     for name, a, b in (("dq", qc.grad, rq), ("dk", kc.grad, rk), ("dv", vc.grad, rv)):
         assert _rel(a.cpu(), b) <= 0.05, (name, _rel(a.cpu(), b))
+
+
+@pytest.mark.parametrize("shape", SHAPES + [(1, 2, 2, 256, 512, 128), (2, 3, 3, 96, 96, 128)])
+@pytest.mark.parametrize("causal", [False, True])
+def test_int8_bwd_ws_bit_identical(lib, shape, causal):
+    """dQ from the dS workspace written by the fused dK+dV kernel (qattn_int8_attn_bwd_ws) against
+    the recomputing dQ kernel (qattn_int8_attn_bwd_ex): same dS_i8 and scales, same operand and MFMA
+    order, so dq, dk, dv agree bit for bit -- over GQA, Sq != Sk, causal and partial workgroups."""
+    from quantizedattention_amd.attention_int8 import _int8_backward, helion_atten_int8_hl_dot_fwd
+    B, Hq, Hkv, Sq, Sk, D = shape
+    q, k, v = _inputs(shape, seed=5)
+    dO = torch.randn((B, Hq, Sq, D), generator=torch.Generator().manual_seed(6)).half().cuda()
+    O, lse, qi, kiT, vi, sq, sk, sv, _, _ = helion_atten_int8_hl_dot_fwd(
+        q.cuda(), k.cuda(), v.cuda(), causal=causal)
+    a = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, causal=causal, kv_heads=Hkv, use_ws=True)
+    b = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, causal=causal, kv_heads=Hkv, use_ws=False)
+    torch.cuda.synchronize()
+    for name, x, y in zip(("dq", "dk", "dv"), a, b):
+        assert torch.isfinite(x).all(), name
+        assert torch.equal(x, y), (name, (x.float() - y.float()).abs().max().item())

@@ -17,7 +17,7 @@ from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp
 
 name = sys.argv[1]
 if name == "int8_all":  # every int8 attention kernel once per rep, in step order
-    names = ["int8_fwd", "int8_dkdv", "int8_dq"]
+    names = ["int8_fwd", "int8_dkdv_ws", "int8_dqw", "int8_dkdv", "int8_dq"]
 else:
     names = [name]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
@@ -42,6 +42,7 @@ qb, kb, ob = (torch.empty((N, D), dtype=torch.bfloat16, device="cuda") for _ in 
 for a_, b_ in ((qi, qb), (ki, kb), (dOi, ob)):
     _lib.call("qattn_i8_to_bf16", P(a_), P(b_), N * D, st)
 dq, dk, dv = (torch.empty_like(q) for _ in range(3))
+ws = torch.empty((_lib.load().qattn_int8_bwd_ws_bytes(B * H, S, S),), dtype=torch.uint8, device="cuda")
 vb = v.bfloat16()
 if name.startswith("bf16"):
     Ob, lseb = helion_atten_bf16_fwd_training(q, k, vb, False)
@@ -55,6 +56,11 @@ for name in [n for _ in range(reps) for n in names]:
     elif name in ("int8_dv", "int8_dk"):
         _lib.call("qattn_" + name.replace("int8_", "int8_bwd_"), P(dOi), P(sdO), P(qi), P(sq), P(ki),
                   P(sk), P(vi), P(sv), P(LD), P(qb), P(ob), P(dk), P(dv), B * H, S, D, qks, sms, st)
+    elif name == "int8_dkdv_ws":
+        _lib.call("qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv),
+                  P(LD), P(qb), P(ob), P(dk), P(dv), P(ws), B * H, S, D, qks, sms, st)
+    elif name == "int8_dqw":
+        _lib.call("qattn_int8_bwd_dq_ws", P(kb), P(sk), P(dq), P(ws), B * H, S, D, sms, st)
     elif name == "int8_dq":
         _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
                   P(kb), P(dq), B * H, S, D, qks, sms, st)

@@ -24,8 +24,10 @@ PROF = os.path.join(ROOT, "profiles")
 # bench.py kernel keys -> normalised rocprof kernel-name patterns (D = 128 instantiations)
 KEYS = {
     "int8_attn_fwd_kernel": r"int8_attn_fwd_kernel(<128(,0)?>|ILi128ELi0E|ILi128EE)",
-    "int8_bwd_dkdv_kernel<dK+dV>": r"int8_bwd_kernel(<128,3>|ILi128ELi3E)",
-    "int8_bwd_dq_kernel": r"int8_bwd_kernel(<128,2>|ILi128ELi2E)",
+    "int8_bwd_dkdv_kernel<dK+dV>": r"int8_bwd_kernel(<128, ?3, ?false, ?false>|ILi128ELi3ELb0ELb0E)",
+    "int8_bwd_dq_kernel": r"int8_bwd_kernel(<128, ?2|ILi128ELi2E)",
+    "int8_bwd_dkdv_kernel<dK+dV, dS out>": r"int8_bwd_kernel(<128, ?3, ?false, ?true>|ILi128ELi3ELb0ELb1E)",
+    "int8_bwd_dqw_kernel": r"int8_bwd_dqw_kernel(<128|ILi128E)",
 }
 SIMDS_PER_XCD = 32 * 4
 # GRBM_GUI_ACTIVE is summed over the 8 XCDs; SQ_VALU_MFMA_BUSY_CYCLES counts 32 busy SIMD-cycles per
