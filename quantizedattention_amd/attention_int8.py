@@ -160,8 +160,13 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
     ws_bytes = _lib.load().qattn_int8_bwd_ws_bytes(B * H, S, Sk)
     if use_ws is None:
         use_ws = 0 <= ws_bytes <= WS_MAX_BYTES
+    ws = None
     if use_ws and ws_bytes > 0:
-        ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
+        try:
+            ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
+        except torch.cuda.OutOfMemoryError:
+            ws = None   # no room for the workspace: recompute dS in the dQ pass (same results)
+    if ws is not None:
         _lib.call("qattn_int8_attn_bwd_ws", *common, _lib.ptr(ws), *shape)
     else:
         _lib.call("qattn_int8_attn_bwd_ex", *common, *shape)

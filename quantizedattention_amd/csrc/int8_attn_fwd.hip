@@ -32,6 +32,7 @@
 // exceeds it by more than THR = 8 (log2 units); P_i8 depends only on S - rowmax(tile), O and l share
 // the (possibly stale) reference, so O / l is unchanged up to rounding and operands stay <= 2^8.
 #include <climits>
+#include <type_traits>
 
 #include "common.h"
 
@@ -39,6 +40,9 @@ namespace qattn {
 
 #ifndef QA_FWD_OCC
 #define QA_FWD_OCC 3
+#endif
+#ifndef QA_FWD_UNROLL
+#define QA_FWD_UNROLL 0
 #endif
 
 template <int D>
@@ -210,11 +214,17 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
   _Float16 m = (_Float16)(-INFINITY);
   float l = 0.f;  // per-lane partial (this lane's key half); the reference's l = 1 is wiped by r = 0
 
-  auto slot_of = [&](int t) -> const char* { return smem + (STREAM ? (t & 3) : 0) * C::SLOT; };
+  // ring slot of a tile: a runtime tile index (slot t & 3), or, with QA_FWD_UNROLL, the slot as a
+  // compile-time constant (every LDS offset becomes a lane-constant VGPR plus an immediate)
+  auto slot_idx = [](auto t) -> int {
+    if constexpr (std::is_integral_v<decltype(t)>) return t & 3;
+    else return decltype(t)::value;
+  };
+  auto slot_of = [&](auto t) -> const char* { return smem + (STREAM ? slot_idx(t) : 0) * C::SLOT; };
 
   // S^T tile t into an int32 accumulator: fragment loads and MFMAs separately, so the K loads of
   // tile t+1 can be issued ahead of the V-operand loads of tile t
-  auto qk_load = [&](int t, v4i* kf) {
+  auto qk_load = [&](auto t, v4i* kf) {
     const char* kl = slot_of(t);
 #pragma unroll
     for (int s = 0; s < C::NKS; ++s) {
@@ -345,7 +355,7 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
 
   // O^T += Vdq^T P^T for tile t: operand loads (issued early, consumed after QK(t+1) and SM2(t))
   // and the MFMAs
-  auto pv_load = [&](int t, v8h* va) {
+  auto pv_load = [&](auto t, v8h* va) {
     const char* vl = slot_of(t);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -410,7 +420,9 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
 #else
 #define QA_STAMP(k)
 #endif
-  for (int t = 0; t < nt; ++t) {
+  // one tile: SLc holds tile t, NXc tile t+1 (the slot after the last one holds a clamped duplicate),
+  // DMc is the slot the DMA of tile t+3 refills
+  auto step = [&](auto SLc, auto NXc, auto DMc, int t) {
     QA_STAMP(0)
     if constexpr (STREAM) {
 #if defined(QA_FWD_NOBAR)
@@ -419,13 +431,13 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
 #endif
       QA_STAMP(1)
-      dma.issue(smem_lds + ((t + 3) & 3) * C::SLOT, min(t + 3, nt - 1));
+      dma.issue(smem_lds + slot_idx(DMc) * C::SLOT, min(t + 3, nt - 1));
     }
     if (active) {
       const int tn = min(t + 1, nt - 1);
       const float cn = cq * (float)sk_lds[tn];
       v4i kf[C::NKS];
-      qk_load(tn, kf);
+      qk_load(NXc, kf);
       v8h va[2 * C::NDB];
 #if defined(QA_FWD_VLATE)
       // the V reads join the LDS queue only after this wave's K reads have returned, so the K reads
@@ -433,10 +445,10 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       // behind 4 x 16 transposed V reads
       const v16i nacc = qk_mma(kf);
       __builtin_amdgcn_sched_barrier(0);
-      pv_load(t, va);
+      pv_load(SLc, va);
       __builtin_amdgcn_sched_barrier(0);
 #else
-      pv_load(t, va);
+      pv_load(SLc, va);
 #endif
 #if defined(QA_FWD_SB)
       __builtin_amdgcn_sched_barrier(0);   // LDS reads issue first; the softmax VALU covers their latency
@@ -471,7 +483,22 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       }
       QA_STAMP(6)
     }
+    };
+#if QA_FWD_UNROLL
+  static_assert(C::NSLOT == 4, "unrolled for the 4-slot ring");
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  for (int t = 0; t < nt; t += 4) {
+    step(I0{}, I1{}, I3{}, t);
+    if (t + 1 < nt) step(I1{}, I2{}, I0{}, t + 1);
+    if (t + 2 < nt) step(I2{}, I3{}, I1{}, t + 2);
+    if (t + 3 < nt) step(I3{}, I0{}, I2{}, t + 3);
   }
+#else
+  for (int t = 0; t < nt; ++t) step(t, t + 1, t + 3, t);
+#endif
 #undef QA_STAMP
   if constexpr (STREAM) vmcnt_wait_all();
   __syncthreads();   // every wave is done with the ring: its slots become the output staging area
