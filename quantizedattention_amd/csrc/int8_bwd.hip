@@ -173,6 +173,7 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #define QA_DKV_STAGGER 1
 #endif
 
+
 template <int D, int ROLE>
 struct BwdCfg {
   using C = I8BwdCfg<D>;
@@ -408,6 +409,18 @@ void int8_bwd_kernel(
   // per-tile quantisation of X into the two bf16 B operands, scaled by so (the other operand's
   // per-tile scale)
   auto quantise = [&](const float* X, float so, v8bf* op) {
+#if defined(QA_DKV_AB)   // timing ablation only (wrong results): no quantisation arithmetic
+    if (X != nullptr) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        v4u w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = pk_bf16(X[8 * s2 + 2 * j], X[8 * s2 + 2 * j + 1]);
+        op[s2] = __builtin_bit_cast(v8bf, w);
+      }
+      return;
+    }
+#endif
     const float xmax = wave_max_dpp(max16_abs3(X));
     const float sx = xmax * (1.0f / 127.0f);
     const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
@@ -963,8 +976,9 @@ extern "C" int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const 
                                       int group, int causal, int head_dim, float qks, float sms,
                                       void* stream) {
   if (ws == nullptr) return 1;
-  return int8_bwd_launch(16 | 32, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, k_bf, dO_bf, dq,
-                         dk, dv, bh, sq_tok, sk_tok, group, causal, head_dim, qks, sms, stream, ws);
+  return int8_bwd_launch(16 | 32, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD,
+                         q_bf, k_bf, dO_bf, dq, dk, dv, bh, sq_tok, sk_tok, group, causal, head_dim, qks,
+                         sms, stream, ws);
 }
 
 // The two parts of qattn_int8_attn_bwd_ws, launchable alone (per-kernel timing).
@@ -975,8 +989,9 @@ extern "C" int qattn_int8_bwd_dkdv_ws(const void* dO_i8, const void* sdO, const 
                                       long bh, long seq, int head_dim, float qks, float sms,
                                       void* stream) {
   if (ws == nullptr) return 1;
-  return int8_bwd_launch(16, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf, nullptr, dO_bf,
-                         nullptr, dk, dv, bh, seq, seq, 1, 0, head_dim, qks, sms, stream, ws);
+  return int8_bwd_launch(16, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf,
+                         nullptr, dO_bf, nullptr, dk, dv, bh, seq, seq, 1, 0, head_dim, qks, sms, stream,
+                         ws);
 }
 extern "C" int qattn_int8_bwd_dq_ws(const void* k_bf, const void* sk, void* dq, void* ws, long bh,
                                     long seq, int head_dim, float sms, void* stream) {
