@@ -633,7 +633,7 @@ struct DqwCfg {
   static constexpr int WAVES = QA_DQW_WAVES;
   static constexpr int T16 = 64 * D;               // bf16 k image of a 32-key tile (L2-resident)
   static constexpr int NSLOT = 4;                  // k image ring: 3 tiles ahead
-  static constexpr int RSLOT = WAVES == 8 ? 5 : 10;   // record ring (HBM stream)
+  static constexpr int RSLOT = WAVES >= 16 ? 4 : WAVES == 8 ? 5 : 10;   // record ring (HBM stream)
   static constexpr int REC = WAVES * 1024;         // the waves' dS records of one tile
   static constexpr int RBASE = NSLOT * T16;
   static constexpr int NP16 = T16 / 1024;
@@ -643,7 +643,7 @@ struct DqwCfg {
 };
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(64 * QA_DQW_WAVES, 2) void int8_bwd_dqw_kernel(
+__global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void int8_bwd_dqw_kernel(
     const int8_t* __restrict__ ds8, const float* __restrict__ sds, const __bf16* __restrict__ kbf,
     const _Float16* __restrict__ sk, _Float16* __restrict__ dq, int BH, int Sq, int Sk, int G,
     float sms) {

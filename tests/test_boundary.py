@@ -134,3 +134,14 @@ def test_oracle_not_imported_by_product():
     for p in (ROOT / "quantizedattention_amd").rglob("*.py"):
         src = p.read_text()
         assert not re.search(r"^\s*(from|import)\s+oracle\b", src, flags=re.M), p
+
+
+@pytest.mark.skipif(not LIB.exists(), reason="libqattn.so not built")
+def test_bwd_workspace_size():
+    """qattn_int8_bwd_ws_bytes (host-only): 1 KiB record + 4 B scale per (head, q-tile, k-tile)."""
+    from quantizedattention_amd import _lib
+    lib = _lib.load()
+    assert lib.qattn_int8_bwd_ws_bytes(4 * 32, 4096, 4096) == 128 * 128 * 128 * 1028
+    assert lib.qattn_int8_bwd_ws_bytes(6, 96, 160) == 6 * 3 * 5 * 1028
+    assert lib.qattn_int8_bwd_ws_bytes(2, 100, 64) == -1          # tokens not a multiple of 32
+    assert lib.qattn_int8_bwd_ws_bytes(0, 64, 64) == 0
