@@ -204,6 +204,18 @@ int qattn_jvp_fwd_x3(const void* q_hi, const void* q_lo, const void* k_hi, const
                      void* out, void* tout, void* lse, long bh, long sq, long sk, int head_dim,
                      float qks, float sm, void* stream);
 
+/* qattn_jvp_fwd / qattn_jvp_fwd_x3 with grouped-query attention (SURVEY §8f N2 for the JVP path):
+ * bh = batch * query heads; k, v, tk, tv have bh / group heads (query head h reads key/value head
+ * h / group).  The reference's JVP kernel takes equal head counts (jvp:33-41). */
+int qattn_jvp_fwd_ex(const void* q, const void* k, const void* v, const void* tq, const void* tk,
+                     const void* tv, void* out, void* tout, void* lse, long bh, long sq, long sk,
+                     int group, int head_dim, float qks, float sm, void* stream);
+int qattn_jvp_fwd_x3_ex(const void* q_hi, const void* q_lo, const void* k_hi, const void* k_lo,
+                        const void* v_hi, const void* v_lo, const void* tq_hi, const void* tq_lo,
+                        const void* tk_hi, const void* tk_lo, const void* tv_hi, const void* tv_lo,
+                        void* out, void* tout, void* lse, long bh, long sq, long sk, int group,
+                        int head_dim, float qks, float sm, void* stream);
+
 /* hi = bf16(x), lo = bf16(x - hi) (both round-to-nearest-even) for n fp32 elements, n % 4 == 0. */
 int qattn_split_bf16(const void* x, void* hi, void* lo, long n, void* stream);
 

@@ -51,6 +51,9 @@ SIGNATURES = {
     "qattn_bf16_bwd": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
     "qattn_jvp_fwd": [_vp] * 9 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
     "qattn_jvp_fwd_x3": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_float, _c_float, _vp],
+    "qattn_jvp_fwd_ex": [_vp] * 9 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
+    "qattn_jvp_fwd_x3_ex": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float,
+                                         _vp],
     "qattn_split_bf16": [_vp, _vp, _vp, _c_long, _vp],
     "qattn_mxfp4_quant_rows": [_vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_mxfp4_quant_vt": [_vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],

@@ -52,6 +52,11 @@ def helion_attention_jvp_forward_fp32(q_fp32_input, k_fp32_input, v_fp32_input,
         if t.shape != ref.shape:
             raise _lib.QAttnError("qattn jvp: tangents must have the primals' shapes")
     B, H, S, D = q_fp32_input.shape
+    # grouped-query attention (SURVEY §8f N2 extension): k, v may have fewer heads than q
+    Hkv = k_head
+    if k_batch != batch or v_batch != batch or v_head != Hkv or H % Hkv != 0:
+        raise _lib.QAttnError("qattn jvp: k and v need q's batch and a head count dividing q's")
+    group = H // Hkv
     dev = q_fp32_input.device
     O = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
     tO = torch.empty_like(O)
@@ -63,9 +68,9 @@ def helion_attention_jvp_forward_fp32(q_fp32_input, k_fp32_input, v_fp32_input,
         if k_tokens % 64:
             raise _lib.QAttnError("qattn jvp: k tokens must be a multiple of 64 for bf16 inputs")
         q, k, v, tq, tk, tv = (t.contiguous() for t in ins)
-        _lib.call("qattn_jvp_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(tq), _lib.ptr(tk),
-                  _lib.ptr(tv), _lib.ptr(O), _lib.ptr(tO), _lib.ptr(lse), B * H, S, k_tokens, D, 0, qks,
-                  sm, st)
+        _lib.call("qattn_jvp_fwd_ex", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(tq), _lib.ptr(tk),
+                  _lib.ptr(tv), _lib.ptr(O), _lib.ptr(tO), _lib.ptr(lse), B * H, S, k_tokens, group, D,
+                  qks, sm, st)
         return O, tO, lse
     imgs = []
     for t in ins:
@@ -74,8 +79,8 @@ def helion_attention_jvp_forward_fp32(q_fp32_input, k_fp32_input, v_fp32_input,
         lo = torch.empty_like(hi)
         _lib.call("qattn_split_bf16", _lib.ptr(x), _lib.ptr(hi), _lib.ptr(lo), x.numel(), st)
         imgs += [hi, lo]
-    _lib.call("qattn_jvp_fwd_x3", *(_lib.ptr(t) for t in imgs), _lib.ptr(O), _lib.ptr(tO), _lib.ptr(lse),
-              B * H, S, k_tokens, D, qks, sm, st)
+    _lib.call("qattn_jvp_fwd_x3_ex", *(_lib.ptr(t) for t in imgs), _lib.ptr(O), _lib.ptr(tO),
+              _lib.ptr(lse), B * H, S, k_tokens, group, D, qks, sm, st)
     return O, tO, lse
 
 

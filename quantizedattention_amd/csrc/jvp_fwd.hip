@@ -76,7 +76,7 @@ struct JvpArgs {
   float* out;
   float* tout;
   float* lse;
-  int BH, Sq, Sk;
+  int BH, Sq, Sk, G;   // G: query heads per key/value head (grouped-query attention)
   float qks, sm;
 };
 
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
   for (int b = 0; b < C::NDB; ++b) { o[b] = v16f{}; ab[b] = v16f{}; }
   float m = -INFINITY, l = 0.f, racc = 0.f;   // jvp:130-134
 
-  const long kv0 = (long)bh * Sk * D;
+  const long kv0 = (long)(bh / a.G) * Sk * D;
   const int nkb = Sk / C::KB;
   // stage layout: [K x NI][tK x NI][V x NI][tV x NI]
   auto stage = [&](int kb, int buf) {
@@ -270,7 +270,7 @@ static int launch_jvp(const JvpArgs& a, long bh, long sq, hipStream_t st) {
 }
 
 static JvpArgs jvp_args(const void* const* img, void* out, void* tout, void* lse, long bh, long sq,
-                        long sk, float qks, float sm, int nimg) {
+                        long sk, int group, float qks, float sm, int nimg) {
   JvpArgs a;
   const __bf16** dst[6] = {a.q, a.k, a.v, a.tq, a.tk, a.tv};
   for (int t = 0; t < 6; ++t) {
@@ -283,20 +283,47 @@ static JvpArgs jvp_args(const void* const* img, void* out, void* tout, void* lse
   a.BH = (int)bh;
   a.Sq = (int)sq;
   a.Sk = (int)sk;
+  a.G = group;
   a.qks = qks;
   a.sm = sm;
   return a;
 }
 
+extern "C" int qattn_jvp_fwd_ex(const void* q, const void* k, const void* v, const void* tq,
+                                const void* tk, const void* tv, void* out, void* tout, void* lse, long bh,
+                                long sq, long sk, int group, int head_dim, float qks, float sm,
+                                void* stream) {
+  if (sq % 32 != 0 || sk % 64 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128))
+    return 1;
+  if (bh == 0 || sq == 0) return 0;
+  const void* img[6] = {q, k, v, tq, tk, tv};
+  const JvpArgs a = jvp_args(img, out, tout, lse, bh, sq, sk, group, qks, sm, 1);
+  hipStream_t st = (hipStream_t)stream;
+  return head_dim == 128 ? launch_jvp<128, false>(a, bh, sq, st) : launch_jvp<64, false>(a, bh, sq, st);
+}
+
 extern "C" int qattn_jvp_fwd(const void* q, const void* k, const void* v, const void* tq, const void* tk,
                              const void* tv, void* out, void* tout, void* lse, long bh, long sq, long sk,
                              int head_dim, int flags, float qks, float sm, void* stream) {
-  if (flags != 0 || sq % 32 != 0 || sk % 64 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  if (flags != 0) return 1;
+  return qattn_jvp_fwd_ex(q, k, v, tq, tk, tv, out, tout, lse, bh, sq, sk, 1, head_dim, qks, sm, stream);
+}
+
+extern "C" int qattn_jvp_fwd_x3_ex(const void* q_hi, const void* q_lo, const void* k_hi, const void* k_lo,
+                                   const void* v_hi, const void* v_lo, const void* tq_hi,
+                                   const void* tq_lo, const void* tk_hi, const void* tk_lo,
+                                   const void* tv_hi, const void* tv_lo, void* out, void* tout, void* lse,
+                                   long bh, long sq, long sk, int group, int head_dim, float qks, float sm,
+                                   void* stream) {
+  if (sq % 32 != 0 || sk % 32 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128))
+    return 1;
   if (bh == 0 || sq == 0) return 0;
-  const void* img[6] = {q, k, v, tq, tk, tv};
-  const JvpArgs a = jvp_args(img, out, tout, lse, bh, sq, sk, qks, sm, 1);
+  const void* img[12] = {q_hi, q_lo, k_hi, k_lo, v_hi, v_lo, tq_hi, tq_lo, tk_hi, tk_lo, tv_hi, tv_lo};
+  const JvpArgs a = jvp_args(img, out, tout, lse, bh, sq, sk, group, qks, sm, 2);
   hipStream_t st = (hipStream_t)stream;
-  return head_dim == 128 ? launch_jvp<128, false>(a, bh, sq, st) : launch_jvp<64, false>(a, bh, sq, st);
+  return head_dim == 128 ? launch_jvp<128, true>(a, bh, sq, st) : launch_jvp<64, true>(a, bh, sq, st);
 }
 
 extern "C" int qattn_jvp_fwd_x3(const void* q_hi, const void* q_lo, const void* k_hi, const void* k_lo,
@@ -304,12 +331,8 @@ extern "C" int qattn_jvp_fwd_x3(const void* q_hi, const void* q_lo, const void* 
                                 const void* tk_hi, const void* tk_lo, const void* tv_hi, const void* tv_lo,
                                 void* out, void* tout, void* lse, long bh, long sq, long sk, int head_dim,
                                 float qks, float sm, void* stream) {
-  if (sq % 32 != 0 || sk % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  if (bh == 0 || sq == 0) return 0;
-  const void* img[12] = {q_hi, q_lo, k_hi, k_lo, v_hi, v_lo, tq_hi, tq_lo, tk_hi, tk_lo, tv_hi, tv_lo};
-  const JvpArgs a = jvp_args(img, out, tout, lse, bh, sq, sk, qks, sm, 2);
-  hipStream_t st = (hipStream_t)stream;
-  return head_dim == 128 ? launch_jvp<128, true>(a, bh, sq, st) : launch_jvp<64, true>(a, bh, sq, st);
+  return qattn_jvp_fwd_x3_ex(q_hi, q_lo, k_hi, k_lo, v_hi, v_lo, tq_hi, tq_lo, tk_hi, tk_lo, tv_hi, tv_lo,
+                             out, tout, lse, bh, sq, sk, 1, head_dim, qks, sm, stream);
 }
 
 extern "C" int qattn_split_bf16(const void* x, void* hi, void* lo, long n, void* stream) {

@@ -85,3 +85,32 @@ def test_jvp_autograd_function_forward_mode(lib, dtype):
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert (O.cpu() - Ot).abs().max().item() <= tol
     assert (tO.cpu() - tOt).abs().max().item() <= tol * max(1.0, tOt.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(1, 4, 2, 128, 128, 128), (2, 6, 3, 64, 192, 64)])
+def test_jvp_grouped_query(lib, dtype, shape):
+    """Grouped-query JVP (extension, SURVEY §8f N2): query head h reads key/value head h // G.
+    Bit-identical to the same call with k, v, tk, tv expanded to every query head, and within the
+    mode's tolerance of torch.func.jvp on the expanded fp32 problem ("parity unpinned": the
+    reference's JVP kernel has no grouped shapes)."""
+    from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp32
+    B, H, Hkv, Sq, Sk, D = shape
+    g = torch.Generator().manual_seed(11)
+    q, tq = (torch.randn((B, H, Sq, D), generator=g) for _ in range(2))
+    k, v, tk, tv = (torch.randn((B, Hkv, Sk, D), generator=g) for _ in range(4))
+    dev = lambda t: t.to(dtype).cuda()  # noqa: E731
+    rep = lambda t: t.repeat_interleave(H // Hkv, dim=1)  # noqa: E731
+    O, tO, lse = helion_attention_jvp_forward_fp32(dev(q), dev(k), dev(v), dev(tq), dev(tk), dev(tv))
+    Oe, tOe, lsee = helion_attention_jvp_forward_fp32(dev(q), dev(rep(k)), dev(rep(v)), dev(tq),
+                                                      dev(rep(tk)), dev(rep(tv)))
+    torch.cuda.synchronize()
+    assert torch.equal(O, Oe) and torch.equal(tO, tOe) and torch.equal(lse, lsee)
+    f = lambda a, b, c: torch.softmax(a @ b.transpose(-1, -2) / D ** 0.5, -1) @ c  # noqa: E731
+    qr, kr, vr = (t.to(dtype).double() for t in (q, rep(k), rep(v)))
+    tqr, tkr, tvr = (t.to(dtype).double() for t in (tq, rep(tk), rep(tv)))
+    Or, tOr = torch.func.jvp(f, (qr, kr, vr), (tqr, tkr, tvr))
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert (O.cpu().double() - Or).abs().max().item() <= tol
+    scale = max(1.0, tOr.abs().max().item())
+    assert (tO.cpu().double() - tOr).abs().max().item() <= tol * scale
