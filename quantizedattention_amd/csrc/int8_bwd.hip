@@ -172,6 +172,10 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #ifndef QA_DKV_STAGGER
 #define QA_DKV_STAGGER 1
 #endif
+// cache policy of the dS record stores (builtin aux: 2 = nt, 16 = sc1)
+#ifndef QA_WS_STORE_AUX
+#define QA_WS_STORE_AUX 0
+#endif
 
 
 template <int D, int ROLE>
@@ -490,7 +494,7 @@ void int8_bwd_kernel(
       const int nqt = Smod / 32, nkt = Sx / 32;
       const unsigned rel = (unsigned)(t * nkt + x0 / 32);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, bytes), ws_rsrc, 16 * lane,
-                                             (int)(rel * 1024u), 0);
+                                             (int)(rel * 1024u), QA_WS_STORE_AUX);
       (void)nqt;
       if (lane == 0) sds_lds[wave * nt + t] = sx;   // written out after the loop
     }
@@ -628,6 +632,9 @@ void int8_bwd_kernel(
 #ifndef QA_DQW_WAVES
 #define QA_DQW_WAVES 8
 #endif
+#ifndef QA_DQW_NT
+#define QA_DQW_NT 1
+#endif
 template <int D>
 struct DqwCfg {
   static constexpr int WAVES = QA_DQW_WAVES;
@@ -685,8 +692,12 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
 #pragma unroll
     for (int i = 0; i < W::IPK; ++i) dma16_buf(krsrc[i], kvoff[i], (unsigned)min(t, nt - 1) * 64u * D, sl + klds[i]);
   };
-  auto issue_r = [&](int t) {
+  auto issue_r = [&](int t) {   // each record is read once: non-temporal
+#if QA_DQW_NT
+    dma16_buf_nt(rrsrc, 16u * lane, (unsigned)min(t, nt - 1) * 1024u,
+#else
     dma16_buf(rrsrc, 16u * lane, (unsigned)min(t, nt - 1) * 1024u,
+#endif
               smem_lds + W::RBASE + (t % W::RSLOT) * W::REC + wave * 1024);
   };
 #pragma unroll

@@ -128,3 +128,19 @@ def test_int8_bwd_ws_bit_identical(lib, shape, causal):
     for name, x, y in zip(("dq", "dk", "dv"), a, b):
         assert torch.isfinite(x).all(), name
         assert torch.equal(x, y), (name, (x.float() - y.float()).abs().max().item())
+
+
+def test_int8_bwd_ws_bit_identical_large(lib):
+    """The same bit-identity at a long sequence, (1, 8, 4096, 128): 128 key tiles per head, every
+    workspace record written by a different (key tile, query tile) pair of waves."""
+    from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward
+    g = torch.Generator(device="cuda").manual_seed(7)
+    q, k, v = (torch.randn((1, 8, 4096, 128), device="cuda", generator=g).half() for _ in range(3))
+    dO = (torch.randn((1, 8, 4096, 128), device="cuda", generator=g) * 1e-3).half()
+    O, lse, qi, kiT, vi, sq, sk, sv, _, qb, kb = _int8_forward(q, k, v, smooth=True, images=True)
+    a = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb, kb, use_ws=True)
+    b = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb, kb, use_ws=False)
+    torch.cuda.synchronize()
+    for name, x, y in zip(("dq", "dk", "dv"), a, b):
+        assert torch.isfinite(x).all() and x.abs().max().item() > 0, name
+        assert torch.equal(x, y), name
