@@ -4,7 +4,9 @@ The drop-in modules (attention_int8 / attention_bf16 / attention_jvp / attention
 C-ABI library directly.  This module registers the same computations as dispatcher operators, so
 that graph capture (``torch.compile``, ``torch.export``, FX tracing) sees one opaque node per
 kernel sequence instead of breaking the graph at a ctypes call.  Each operator has a fake (meta)
-implementation giving output shapes and dtypes without running anything.
+implementation giving output shapes and dtypes without running anything; ``int8_fwd`` and
+``bf16_fwd`` carry autograd rules (their backward operators), so compiled training steps
+differentiate through them.
 
     torch.ops.qattn.int8_fwd(q, k, v, smooth, causal) -> (O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
     torch.ops.qattn.int8_bwd(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, causal, kv_heads)
@@ -74,6 +76,29 @@ def _(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, causal, kv_heads):
             O.new_empty((B, kv_heads, Sk, D), dtype=torch.float16))
 
 
+def _int8_setup(ctx, inputs, output):
+    q, k, v, smooth, causal = inputs
+    O, lse, q_i8, k_i8, v_i8, sq, sk, sv = output
+    ctx.save_for_backward(O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
+    ctx.causal, ctx.kv_heads = causal, k.shape[1]
+    ctx.dtypes = (q.dtype, k.dtype, v.dtype)
+
+
+def _int8_backward_rule(ctx, dO, *_unused):
+    # gradient of O only (the quantised outputs are not differentiable, int8:52-56); k smoothing
+    # adds no gradient (softmax-invariant), so the same backward serves smooth and plain forwards
+    O, lse, q_i8, k_i8, v_i8, sq, sk, sv = ctx.saved_tensors
+    if dO is None:
+        return None, None, None, None, None
+    dq, dk, dv = int8_bwd(dO.to(torch.float16), q_i8, sq, k_i8, sk, v_i8, sv, O, lse, ctx.causal,
+                          ctx.kv_heads)
+    qd, kd, vd = ctx.dtypes
+    return dq.to(qd), dk.to(kd), dv.to(vd), None, None
+
+
+int8_fwd.register_autograd(_int8_backward_rule, setup_context=_int8_setup)
+
+
 # ------------------------------------------------------------------------------------ bf16
 @torch.library.custom_op(f"{_LIB}::bf16_fwd", mutates_args=(), device_types="cuda")
 def bf16_fwd(q: Tensor, k: Tensor, v: Tensor, causal: bool) -> Tuple[Tensor, Tensor]:
@@ -99,6 +124,24 @@ def bf16_bwd(q: Tensor, k: Tensor, v: Tensor, O: Tensor, lse: Tensor, causal: bo
 def _(q, k, v, O, lse, causal, dO):
     return (q.new_empty(q.shape, dtype=torch.float32), k.new_empty(k.shape, dtype=torch.float32),
             v.new_empty(v.shape, dtype=torch.float32))
+
+
+def _bf16_setup(ctx, inputs, output):
+    q, k, v, causal = inputs
+    O, lse = output
+    ctx.save_for_backward(q, k, v, O, lse)
+    ctx.causal = causal
+
+
+def _bf16_backward_rule(ctx, dO, _dlse):
+    q, k, v, O, lse = ctx.saved_tensors
+    if dO is None:
+        return None, None, None, None
+    dq, dk, dv = bf16_bwd(q, k, v, O, lse, ctx.causal, dO)
+    return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), None
+
+
+bf16_fwd.register_autograd(_bf16_backward_rule, setup_context=_bf16_setup)
 
 
 # ------------------------------------------------------------------------------------- jvp

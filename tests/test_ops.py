@@ -52,3 +52,27 @@ def test_ops_match_dropins_and_compile(lib):
 
     cf = torch.compile(f, backend="eager", fullgraph=True)
     assert torch.equal(cf(q, k, v), f(q, k, v))
+
+
+@pytest.mark.gpu
+def test_ops_autograd_matches_dropins(lib):
+    """Autograd through torch.ops.qattn.int8_fwd / bf16_fwd equals the drop-in autograd Functions
+    (int8: bit-identical -- the op rebuilds the bf16 images the drop-in forward writes)."""
+    from quantizedattention_amd.attention_bf16 import flash_atten_2_bf16
+    from quantizedattention_amd.attention_int8 import sage_attention_3_int8
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q, k, v = (torch.randn((1, 4, 256, 128), device="cuda", generator=g).half() for _ in range(3))
+    dO = torch.randn((1, 4, 256, 128), device="cuda", generator=g).half()
+    a = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    b = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    torch.ops.qattn.int8_fwd(*a, True, False)[0].backward(dO)
+    sage_attention_3_int8(*b).backward(dO)
+    for x, y in zip(a, b):
+        assert torch.equal(x.grad, y.grad)
+    vb = v.bfloat16()
+    a = [t.clone().requires_grad_(True) for t in (q, k, vb)]
+    b = [t.clone().requires_grad_(True) for t in (q, k, vb)]
+    torch.ops.qattn.bf16_fwd(*a, False)[0].backward(dO.float())
+    flash_atten_2_bf16(*b, False).backward(dO.float())
+    for x, y in zip(a, b):
+        assert torch.equal(x.grad, y.grad)
