@@ -172,7 +172,8 @@ int qattn_f16_to_bf16(const void* x, void* y, long n, void* stream);
 /* Corrected FA2 backward (helion_flash_atten_2_algo_4_bwd, attention_bf16.py:299-448 with SURVEY F3
  * fixed: dS = P*(dP - D), sm_scale, deterministic dq).  q, k f16; v bf16; dO_bf, LD from
  * qattn_bf16_bwd_prep; q_bf, k_bf = qattn_f16_to_bf16 images of q, k.  Out dq [bh*sq, D], dk, dv
- * [bh*sk, D] f32.  Launches one dV, one dK and one dQ kernel.  sq % 32 == 0, sk % 32 == 0. */
+ * [bh*sk, D] f32.  Launches one fused dK+dV kernel and one dQ kernel.  sq % 32 == 0,
+ * sk % 32 == 0. */
 int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
                    const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh, long sq,
                    long sk, int head_dim, int causal, float qks, float sms, void* stream);
@@ -182,6 +183,13 @@ int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_b
 int qattn_bf16_bwd_ex(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
                       const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh, long sq,
                       long sk, int group, int causal, int head_dim, float qks, float sms, void* stream);
+
+/* qattn_bf16_bwd_ex with separate dV and dK kernels (each recomputes S; two waves per SIMD each):
+ * bit-identical dk, dv to the fused kernel; kept for the parity test and as a timing reference. */
+int qattn_bf16_bwd_split_ex(const void* q, const void* k, const void* v, const void* dO_bf,
+                            const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
+                            void* dv, long bh, long sq, long sk, int group, int causal, int head_dim,
+                            float qks, float sms, void* stream);
 
 /* ---------------------------------------------------------------- JVP (attention_jvp.py) */
 

@@ -46,6 +46,8 @@ SIGNATURES = {
     "qattn_bf16_fwd_ex": [_vp] * 5 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
     "qattn_bf16_bwd_ex": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                         _c_float, _vp],
+    "qattn_bf16_bwd_split_ex": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int,
+                                              _c_float, _c_float, _vp],
     "qattn_bf16_bwd_prep": [_vp] * 5 + [_c_long, _c_long, _c_int, _vp],
     "qattn_f16_to_bf16": [_vp, _vp, _c_long, _vp],
     "qattn_bf16_bwd": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],

@@ -72,11 +72,16 @@ __global__ __launch_bounds__(256) void f16_to_bf16_kernel(const _Float16* __rest
 // P = exp2(S*qks - lse) and dS = P*(dP - D) in fp32, then bf16 operands of the accumulating bf16
 // MFMA against the transposed (ds_read_b64_tr_b16) image of the third operand.  Software pipelined by
 // one tile: the products of tile t+1 are issued before the accumulation of tile t, and the fp32
-// P / dS of tile t+1 are computed beside its MFMAs.  Split into three kernels (S recomputed in each)
-// so that each keeps one fp32 accumulator: 2 waves per SIMD instead of 1 for a fused dK+dV.
-enum B16Role { B16_DV = 0, B16_DK = 1, B16_DQ = 2 };
+// P / dS of tile t+1 are computed beside its MFMAs.
+//   ROLE_DKV (bf16_bwd_dkv_kernel below, the default path): X = K, V; Y = {Q fp16 rows, dO bf16
+//             rows, Q bf16 tr image, dO bf16 tr image, LD}; S and P computed once for dV and dK.
+// The split DV + DK kernels (S recomputed in each) remain as qattn_bf16_bwd_split_ex.
+enum B16Role { B16_DV = 0, B16_DK = 1, B16_DQ = 2, B16_DKV = 3 };
 #ifndef QA_B16_DV_OCC
 #define QA_B16_DV_OCC 2
+#endif
+#ifndef QA_B16_SCHED
+#define QA_B16_SCHED 0   // fused dK+dV: explicit MFMA / VALU interleave, bit 1 P wave, bit 2 dS wave
 #endif
 #ifndef QA_B16_DV_NSLOT
 #define QA_B16_DV_NSLOT 3
@@ -89,12 +94,17 @@ struct B16Cfg {
   static constexpr int T16 = 32 * ROWB;                     // one 32-row 16-bit tile
   static constexpr bool TWO = ROLE != B16_DV;               // S and dP
   static constexpr bool HAS_LD = ROLE != B16_DQ;            // {lse, D} per row of the streamed side
-  static constexpr int NREG = TWO ? 3 : 2;                  // 16-bit regions per slot
-  static constexpr int YA = 0, YB = T16, TR = (NREG - 1) * T16, LDO = NREG * T16;
+  static constexpr bool FUSED = ROLE == B16_DKV;
+  // FUSED at D=128: one dO image serves both the row reads (dP) and the tr reads (dV), under the
+  // swizzle b16_csw that is conflict-free for both; D=64 keeps a separate dO tr image
+  static constexpr bool MERGE = FUSED && D == 128;
+  static constexpr int NREG = FUSED ? (MERGE ? 3 : 4) : TWO ? 3 : 2;   // 16-bit regions per slot
+  static constexpr int NROW = FUSED ? 2 : NREG - 1;         // row-read regions come first
+  static constexpr int YA = 0, YB = T16, TR = NROW * T16, TR2 = MERGE ? YB : 3 * T16, LDO = NREG * T16;
   static constexpr int SLOT = NREG * T16 + (HAS_LD ? 256 : 0);
   static constexpr int NSLOT = (ROLE == B16_DV) ? QA_B16_DV_NSLOT : 3;
-  static constexpr int WAVES = 4;
-  static constexpr int XROWS = 32 * WAVES;
+  static constexpr int WAVES = FUSED ? 8 : 4;
+  static constexpr int XROWS = 32 * 4;                      // own rows per workgroup
   static constexpr int NP = T16 / 1024;                     // 1-KiB LDS-DMA pieces per region
   static constexpr int INST = NREG * NP;
   static constexpr int IPW16 = INST / WAVES;
@@ -102,13 +112,20 @@ struct B16Cfg {
   static constexpr int NKS = D / 16;
   static constexpr int NDB = D / 32;
   static constexpr int STAGE = WAVES * RowTile<D, float, 2>::BYTES;   // epilogue in two column halves
-  static constexpr int LDS = (NSLOT * SLOT > STAGE) ? NSLOT * SLOT : STAGE;
+  static constexpr int PBUF = NSLOT * SLOT;                 // FUSED: fp32 P hand-over, 2 tiles
+  static constexpr int PB_WAVE = 32 * 32 * 4, PB_TILE = 4 * PB_WAVE;
+  static constexpr int RING = PBUF + (FUSED ? 2 * PB_TILE : 0);
+  static constexpr int LDS = (RING > STAGE) ? RING : STAGE;
   static_assert(INST % WAVES == 0, "DMA pieces split evenly over the waves");
 };
 template <int D>
 QA_DEVICE int b16_rsw(int row) { return (D == 128) ? (row & 15) : ((row >> 1) & 7); }   // row reads
 template <int D>
 QA_DEVICE int b16_tsw(int row) { return (row & 3) << ((D == 128) ? 2 : 1); }            // tr reads
+// both (D = 128): ds_read_b128 row reads see 16 distinct chunks per 16-lane group, and
+// ds_read_b64_tr_b16 reads of 4 rows x 4 chunks per 32-lane group see 16 distinct chunks; unlike
+// b16_tsw it is not invariant under row += 8, so tr reads keep one offset per 8-row half
+QA_DEVICE int b16_csw(int row) { return (row & 15) ^ ((row & 3) << 2); }
 
 template <int D, int ROLE>
 struct B16Dma {
@@ -117,37 +134,45 @@ struct B16Dma {
   unsigned lds_off[G::IPW16];
   v4u rsrc[G::IPW16];
   v4u ld_rsrc;
-  QA_DEVICE void init(int wave, int lane, int Sy, const char* ya, const char* yb, const char* tr,
-                      const char* ld) {
+  bool ld_on;
+  // region r of a slot is filled from src[r] (row-swizzled for r < NROW, tr-swizzled after; the
+  // merged dO region with b16_csw)
+  QA_DEVICE void init(int wave, int lane, int Sy, const char* const* src, const char* ld) {
     constexpr int RPI = 64 / G::NCH;
 #pragma unroll
     for (int i = 0; i < G::IPW16; ++i) {
       const int p = wave + G::WAVES * i;
       const int r = p / G::NP, q = p % G::NP;
-      const bool is_tr = r == G::NREG - 1;
+      const bool is_tr = r >= G::NROW;
       const int row = q * RPI + lane / G::NCH, c = lane % G::NCH;
-      voff[i] = row * G::ROWB + 16 * (c ^ (is_tr ? b16_tsw<D>(row) : b16_rsw<D>(row)));
+      const int sw = (G::MERGE && r == 1) ? b16_csw(row) : is_tr ? b16_tsw<D>(row) : b16_rsw<D>(row);
+      voff[i] = row * G::ROWB + 16 * (c ^ sw);
       lds_off[i] = r * G::T16 + q * 1024;
-      rsrc[i] = make_rsrc(is_tr ? tr : (r == 0 ? ya : yb), (unsigned)Sy * G::ROWB);
+      rsrc[i] = make_rsrc(src[r], (unsigned)Sy * G::ROWB);
     }
     if constexpr (G::HAS_LD) ld_rsrc = make_rsrc(ld, (unsigned)Sy * 8);
+    ld_on = !G::FUSED || wave == G::WAVES - 1;   // FUSED: one wave brings the {lse, D} rows
   }
   QA_DEVICE void issue(unsigned slot_lds, int t, int lane) const {
 #pragma unroll
     for (int i = 0; i < G::IPW16; ++i)
       dma16_buf(rsrc[i], voff[i], (unsigned)t * G::T16, slot_lds + lds_off[i]);
-    if constexpr (G::HAS_LD) dma4_buf(ld_rsrc, 4 * lane, (unsigned)t * 256, slot_lds + G::LDO);
+    if constexpr (G::HAS_LD)
+      if (ld_on) dma4_buf(ld_rsrc, 4 * lane, (unsigned)t * 256, slot_lds + G::LDO);
   }
 };
 
 template <int D, int ROLE, bool CAUSAL>
-__global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void bf16_bwd_kernel(
-    const _Float16* __restrict__ xa, const __bf16* __restrict__ xb, const _Float16* __restrict__ ya,
-    const __bf16* __restrict__ yb, const __bf16* __restrict__ ytr, const float2* __restrict__ yld,
-    const float2* __restrict__ xld, float* __restrict__ out, int BH, int Sx, int Ny, int ydiv, int Smod,
-    float qks, float osc) {
+__global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void
+bf16_bwd_kernel(const _Float16* __restrict__ xa, const __bf16* __restrict__ xb,
+                const _Float16* __restrict__ ya, const __bf16* __restrict__ yb,
+                const __bf16* __restrict__ ytr, const __bf16* __restrict__ ytr2,
+                const float2* __restrict__ yld, const float2* __restrict__ xld, float* __restrict__ out,
+                float* __restrict__ out2, int BH, int Sx, int Ny, int ydiv, int Smod, float qks,
+                float osc, float osc2) {
   using G = B16Cfg<D, ROLE>;
   constexpr bool TWO = G::TWO;
+  static_assert(!G::FUSED, "B16_DKV runs bf16_bwd_dkv_kernel");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
   int bh, xt;
@@ -172,9 +197,13 @@ __global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void bf16_
   const int nt = t1 - t0;
 
   B16Dma<D, ROLE> dma;
-  dma.init(wave, lane, Ny, reinterpret_cast<const char*>(ya + hy * D),
-           reinterpret_cast<const char*>(yb + hy * D), reinterpret_cast<const char*>(ytr + hy * D),
-           reinterpret_cast<const char*>(yld + hy));
+  {
+    const char* ysrc[4] = {reinterpret_cast<const char*>(ya + hy * D),
+                           reinterpret_cast<const char*>((TWO ? yb : ytr) + hy * D),
+                           reinterpret_cast<const char*>(ytr + hy * D),
+                           reinterpret_cast<const char*>(ytr + hy * D)};
+    dma.init(wave, lane, Ny, ysrc, reinterpret_cast<const char*>(yld + hy));
+  }
   const unsigned smem_lds = lds_addr(smem);
   if (nt > 0) {
 #pragma unroll
@@ -322,6 +351,240 @@ __global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void bf16_
   store_rows<D, float, 2>(acc, osc, smem + wave * RowTile<D, float, 2>::BYTES, out + (hx + x0) * D, lane);
 }
 
+// ---------------------------------------------------------------- fused dK + dV, paired waves
+// One workgroup owns 128 keys of one key/value head; every 32 keys have two waves on one SIMD:
+//   P wave  (waves 0-3, K fp16 fragments):  S -> P = exp2(S*qks - lse) -> dV += dO^T P
+//   dS wave (waves 4-7, V bf16 fragments):  dP -> dS = P (dP - D)     -> dK += Q^T dS
+// The P wave hands its fp32 P of tile t+1 to the dS wave through LDS (two tile buffers); the dS
+// wave uses it one step later, after the ring barrier, so it runs one tile behind.  Both waves
+// carry 16 MFMAs per tile (S or dP, then dV or dK), S and P are computed once, and the P / dS
+// operands and accumulation order are those of the DV / DK kernels: dK, dV are bit-identical to
+// the split path.  Registers: one fragment set + one accumulator per wave, two waves per SIMD.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
+    const _Float16* __restrict__ xa, const __bf16* __restrict__ xb, const _Float16* __restrict__ ya,
+    const __bf16* __restrict__ yb, const __bf16* __restrict__ ytr, const __bf16* __restrict__ ytr2,
+    const float2* __restrict__ yld, const float2* __restrict__ xld, float* __restrict__ out,
+    float* __restrict__ out2, int BH, int Sx, int Ny, int ydiv, int Smod, float qks, float osc,
+    float osc2) {
+  using G = B16Cfg<D, B16_DKV>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
+  int bh, xt;
+  xcd_remap(blockIdx.x, nxb, BH, bh, xt);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool pwave = wave < 4;
+  const int kw = wave & 3;
+  const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int x0 = xt * G::XROWS + kw * 32;
+  const bool active = x0 < Sx;
+  const int xi = x0 + c32;
+  const long hx = (long)bh * Sx, hy = (long)(bh / ydiv) * Ny;
+  int t0 = 0, t1 = Ny / 32;
+  if (CAUSAL && Ny == Smod) t0 = min(t1, (xt * G::XROWS) / 32);   // queries <= every key
+  const int nt = t1 - t0;
+
+  B16Dma<D, B16_DKV> dma;
+  {
+    const char* ysrc[4] = {reinterpret_cast<const char*>(ya + hy * D),
+                           reinterpret_cast<const char*>(yb + hy * D),
+                           reinterpret_cast<const char*>(ytr + hy * D),
+                           reinterpret_cast<const char*>(ytr2 + hy * D)};
+    dma.init(wave, lane, Ny, ysrc, reinterpret_cast<const char*>(yld + hy));
+  }
+  const unsigned smem_lds = lds_addr(smem);
+  if (nt > 0) {
+#pragma unroll
+    for (int i = 0; i < G::NSLOT - 1; ++i) dma.issue(smem_lds + i * G::SLOT, t0 + min(i, nt - 1), lane);
+  }
+  const int xr = min(xi, Sx - 1);
+  // row reads: P wave Q (region YA), dS wave dO (YB); tr reads: P wave dO (TR2), dS wave Q (TR).
+  // troff[s][half][b]: rows 16 s + 8 half + 4 h + i16/4 of the tr read
+  const bool csw_rows = G::MERGE && !pwave, csw_tr = G::MERGE && pwave;
+  int roff[G::NKS], troff[2][2][G::NDB];
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s)
+    roff[s] = c32 * G::ROWB + 16 * ((2 * s + h) ^ (csw_rows ? b16_csw(c32) : b16_rsw<D>(c32)));
+  {
+    const int gg = (lane >> 4) & 1, i16 = lane & 15;
+    const int treg = pwave ? G::TR2 : G::TR;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int row = 16 * s + 8 * hf + 4 * h + (i16 >> 2);
+        const int sw = csw_tr ? b16_csw(row) : b16_tsw<D>(row);
+#pragma unroll
+        for (int b = 0; b < G::NDB; ++b) {
+          const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
+          troff[s][hf][b] = treg + row * G::ROWB + 16 * ((d / 8) ^ sw) + (d % 8) * 2;
+        }
+      }
+  }
+  v16f acc[G::NDB];
+#pragma unroll
+  for (int b = 0; b < G::NDB; ++b) acc[b] = v16f{};
+  // P hand-over: tile t's P of key wave kw at PBUF + ((t - t0) & 1) * PB_TILE + kw * PB_WAVE, lane-
+  // interleaved v4f (conflict-free b128 accesses)
+  auto pbuf = [&](int t) { return reinterpret_cast<v4f*>(smem + G::PBUF + ((t - t0) & 1) * G::PB_TILE +
+                                                         kw * G::PB_WAVE) + lane; };
+  auto slot = [&](auto SLc) -> const char* { return smem + decltype(SLc)::value * G::SLOT; };
+  auto operand = [&](const float* X, v8bf* op) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      v4u w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = pk_bf16(X[8 * s + 2 * j], X[8 * s + 2 * j + 1]);
+      op[s] = __builtin_bit_cast(v8bf, w);
+    }
+  };
+  auto accumulate = [&](auto SLc, const float* X) {
+    const char* base = slot(SLc);
+    v8bf ta[2 * G::NDB];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < G::NDB; ++b)
+        ta[s * G::NDB + b] =
+            __builtin_bit_cast(v8bf, ds_read_tr16_x2(base + troff[s][0][b], base + troff[s][1][b]));
+    v8bf op[2];
+    operand(X, op);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < G::NDB; ++b) acc[b] = mfma_bf16(ta[s * G::NDB + b], op[s], acc[b]);
+  };
+  static_assert(G::NSLOT == 3, "the tile loops below are unrolled for a 3-slot ring");
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  float X[16];
+  auto ring = [&](auto SLc, int t) {
+    ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();   // tile t+1 landed, P(t) written; slot t-1 free
+    dma.issue(smem_lds + ((decltype(SLc)::value + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
+              min(t + G::NSLOT - 1, t1 - 1), lane);
+  };
+  vmem_drain();
+  __syncthreads();
+  if (pwave) {
+    v8h xf[G::NKS];
+#pragma unroll
+    for (int s = 0; s < G::NKS; ++s)
+      xf[s] = *reinterpret_cast<const v8h*>(xa + (hx + xr) * D + 16 * s + 8 * h);
+    auto sprod = [&](auto SLc) {
+      const char* base = slot(SLc);
+      v16f sa{};
+#pragma unroll
+      for (int s = 0; s < G::NKS; ++s) sa = mfma_f16(*reinterpret_cast<const v8h*>(base + G::YA + roff[s]), xf[s], sa);
+      return sa;
+    };
+    // P of tile t in X (as the DV kernel) and in hand-over buffer pb
+    auto pvals = [&](auto SLc, int t, const v16f& sa, v4f* pb) {
+      const int y0 = (32 * t) % Smod;
+      const bool mask = CAUSAL && (y0 <= x0 + 31);
+      const float* ld = reinterpret_cast<const float*>(slot(SLc) + G::LDO);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const v4f a = *reinterpret_cast<const v4f*>(ld + 2 * (8 * g + 4 * h));
+        const v4f b = *reinterpret_cast<const v4f*>(ld + 2 * (8 * g + 4 * h) + 4);
+        const float lse_r[4] = {a[0], a[2], b[0], b[2]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g + j;
+          float sc = sa[i] * qks;                                          // bf16:376-377
+          if (mask && y0 + 8 * g + 4 * h + j - xi <= 0) sc = -128.0f;       // bf16:379-389
+          X[i] = exp2_f32(sc - lse_r[j]);                                  // bf16:392
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pb[64 * g] = v4f{X[4 * g], X[4 * g + 1], X[4 * g + 2], X[4 * g + 3]};
+    };
+    // branch-free: at the last tile P(t1-1) is recomputed into the buffer of tile t+1, whose
+    // previous content P(t-1) the dS wave consumed before this step's barrier
+    auto step = [&](auto SLc, auto NXc, int t) {
+      ring(SLc, t);
+      const v16f sa = sprod(NXc);
+      accumulate(SLc, X);                    // dV += dO^T P(t)
+      pvals(NXc, min(t + 1, t1 - 1), sa, pbuf(t + 1));
+#if QA_B16_SCHED & 1
+      // LDS reads first, the 8 S MFMAs, then each dV MFMA followed by a share of the P VALU
+      __builtin_amdgcn_sched_group_barrier(0x100, 32, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, G::NKS, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+#pragma unroll
+      for (int i = 0; i < 2 * G::NDB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+      }
+#endif
+    };
+    if (nt > 0) {
+      pvals(I0{}, t0, sprod(I0{}), pbuf(t0));
+      for (int t = t0; t < t1; t += 3) {
+        step(I0{}, I1{}, t);
+        if (t + 1 < t1) step(I1{}, I2{}, t + 1);
+        if (t + 2 < t1) step(I2{}, I0{}, t + 2);
+      }
+    }
+  } else {
+    v8bf xf[G::NKS];
+#pragma unroll
+    for (int s = 0; s < G::NKS; ++s)
+      xf[s] = *reinterpret_cast<const v8bf*>(xb + (hx + xr) * D + 16 * s + 8 * h);
+    auto dprod = [&](auto SLc) {
+      const char* base = slot(SLc);
+      v16f pa{};
+#pragma unroll
+      for (int s = 0; s < G::NKS; ++s) pa = mfma_bf16(*reinterpret_cast<const v8bf*>(base + G::YB + roff[s]), xf[s], pa);
+      return pa;
+    };
+    v16f pa = v16f{};
+    auto step = [&](auto SLc, auto NXc, int t) {
+      ring(SLc, t);
+      const v4f* pb = pbuf(t);
+      v4f pv[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pv[g] = pb[64 * g];
+      const v16f pn = dprod(NXc);
+      // dS(t) = P(t) (dP(t) - D), as the DK kernel (F3)
+      const float* ld = reinterpret_cast<const float*>(slot(SLc) + G::LDO);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const v4f a = *reinterpret_cast<const v4f*>(ld + 2 * (8 * g + 4 * h));
+        const v4f b = *reinterpret_cast<const v4f*>(ld + 2 * (8 * g + 4 * h) + 4);
+        const float d_r[4] = {a[1], a[3], b[1], b[3]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) X[4 * g + j] = pv[g][j] * (pa[4 * g + j] - d_r[j]);
+      }
+      accumulate(SLc, X);                    // dK += Q^T dS(t)
+      pa = pn;
+#if QA_B16_SCHED & 2
+      // LDS reads first, then the dP MFMAs of tile t+1 each followed by a share of the dS(t) VALU
+      __builtin_amdgcn_sched_group_barrier(0x100, 36, 0);
+#pragma unroll
+      for (int i = 0; i < G::NKS; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+      }
+#endif
+    };
+    if (nt > 0) {
+      pa = dprod(I0{});
+      for (int t = t0; t < t1; t += 3) {
+        step(I0{}, I1{}, t);
+        if (t + 1 < t1) step(I1{}, I2{}, t + 1);
+        if (t + 2 < t1) step(I2{}, I0{}, t + 2);
+      }
+    }
+  }
+  vmcnt_wait_all();
+  __syncthreads();   // the ring becomes the output staging area
+  if (!active) return;
+  store_rows<D, float, 2>(acc, pwave ? osc2 : osc, smem + wave * RowTile<D, float, 2>::BYTES,
+                          (pwave ? out2 : out) + (hx + x0) * D, lane);
+}
+
 }  // namespace qattn
 
 using namespace qattn;
@@ -352,59 +615,94 @@ extern "C" int qattn_f16_to_bf16(const void* x, void* y, long n, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+struct B16Out {
+  void* out;
+  void* out2;
+  float osc, osc2;
+};
 template <int D, int ROLE, bool CAUSAL>
 static void launch_b16c(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
-                        const void* yld, const void* xld, void* out, long bh, long sx, long ny,
-                        int ydiv, long smod, float qks, float osc, hipStream_t st) {
+                        const void* ytr2, const void* yld, const void* xld, B16Out o, long bh, long sx,
+                        long ny, int ydiv, long smod, float qks, hipStream_t st) {
   using G = B16Cfg<D, ROLE>;
-  hipFuncSetAttribute((const void*)bf16_bwd_kernel<D, ROLE, CAUSAL>,
-                      hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+  auto kern = [] {
+    if constexpr (ROLE == B16_DKV) return bf16_bwd_dkv_kernel<D, CAUSAL>;
+    else return bf16_bwd_kernel<D, ROLE, CAUSAL>;
+  }();
+  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
   const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
-  hipLaunchKernelGGL((bf16_bwd_kernel<D, ROLE, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
+  hipLaunchKernelGGL(kern, dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
                      G::LDS, st, (const _Float16*)xa, (const __bf16*)xb, (const _Float16*)ya,
-                     (const __bf16*)yb, (const __bf16*)ytr, (const float2*)yld, (const float2*)xld,
-                     (float*)out, (int)bh, (int)sx, (int)ny, ydiv, (int)smod, qks, osc);
+                     (const __bf16*)yb, (const __bf16*)ytr, (const __bf16*)ytr2, (const float2*)yld,
+                     (const float2*)xld, (float*)o.out, (float*)o.out2, (int)bh, (int)sx, (int)ny,
+                     ydiv, (int)smod, qks, o.osc, o.osc2);
 }
 template <int D, int ROLE>
 static void launch_b16(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
-                       const void* yld, const void* xld, void* out, long bh, long sx, long ny,
-                       int ydiv, long smod, int causal, float qks, float osc, hipStream_t st) {
+                       const void* ytr2, const void* yld, const void* xld, B16Out o, long bh, long sx,
+                       long ny, int ydiv, long smod, int causal, float qks, hipStream_t st) {
   if (causal)
-    launch_b16c<D, ROLE, true>(xa, xb, ya, yb, ytr, yld, xld, out, bh, sx, ny, ydiv, smod, qks, osc, st);
+    launch_b16c<D, ROLE, true>(xa, xb, ya, yb, ytr, ytr2, yld, xld, o, bh, sx, ny, ydiv, smod, qks, st);
   else
-    launch_b16c<D, ROLE, false>(xa, xb, ya, yb, ytr, yld, xld, out, bh, sx, ny, ydiv, smod, qks, osc, st);
+    launch_b16c<D, ROLE, false>(xa, xb, ya, yb, ytr, ytr2, yld, xld, o, bh, sx, ny, ydiv, smod, qks, st);
 }
 
 // bh = batch * query heads; key/value tensors have bh / group heads of sk rows
 template <int D>
 static void bf16_bwd_d(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
                        const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh,
-                       long sq, long sk, int group, int causal, float qks, float sms, hipStream_t st) {
+                       long sq, long sk, int group, int causal, float qks, float sms, bool split,
+                       hipStream_t st) {
   const long bkv = bh / group, ny = group * sq;
-  // dV: own K / streamed Q rows, dO tr image, LD
-  launch_b16<D, B16_DV>(k, nullptr, q, nullptr, dO_bf, LD, nullptr, dv, bkv, sk, ny, 1, sq, causal, qks,
-                        1.0f, st);
-  // dK: own K, V / streamed Q rows, dO rows, Q bf16 tr image, LD
-  launch_b16<D, B16_DK>(k, v, q, dO_bf, q_bf, LD, nullptr, dk, bkv, sk, ny, 1, sq, causal, qks, sms, st);
+  if (split) {
+    // dV: own K / streamed Q rows, dO tr image, LD
+    launch_b16<D, B16_DV>(k, nullptr, q, nullptr, dO_bf, nullptr, LD, nullptr, {dv, nullptr, 1.0f, 0.f},
+                          bkv, sk, ny, 1, sq, causal, qks, st);
+    // dK: own K, V / streamed Q rows, dO rows, Q bf16 tr image, LD
+    launch_b16<D, B16_DK>(k, v, q, dO_bf, q_bf, nullptr, LD, nullptr, {dk, nullptr, sms, 0.f}, bkv, sk,
+                          ny, 1, sq, causal, qks, st);
+  } else {
+    // dK + dV: own K, V / streamed Q rows, dO rows, Q bf16 tr image, dO bf16 tr image, LD
+    launch_b16<D, B16_DKV>(k, v, q, dO_bf, q_bf, dO_bf, LD, nullptr, {dk, dv, sms, 1.0f}, bkv, sk, ny, 1,
+                           sq, causal, qks, st);
+  }
   // dQ: own Q, dO (+ LD of their rows) / streamed K rows, V rows, K bf16 tr image
-  launch_b16<D, B16_DQ>(q, dO_bf, k, v, k_bf, nullptr, LD, dq, bh, sq, sk, group, sk, causal, qks, sms,
-                        st);
+  launch_b16<D, B16_DQ>(q, dO_bf, k, v, k_bf, nullptr, nullptr, LD, {dq, nullptr, sms, 0.f}, bh, sq, sk,
+                        group, sk, causal, qks, st);
 }
 
-extern "C" int qattn_bf16_bwd_ex(const void* q, const void* k, const void* v, const void* dO_bf,
-                                 const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
-                                 void* dv, long bh, long sq, long sk, int group, int causal,
-                                 int head_dim, float qks, float sms, void* stream) {
+static int bf16_bwd_entry(const void* q, const void* k, const void* v, const void* dO_bf,
+                          const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
+                          void* dv, long bh, long sq, long sk, int group, int causal, int head_dim,
+                          float qks, float sms, bool split, void* stream) {
   if (sq % 32 != 0 || sk % 32 != 0 || group < 1 || bh % group != 0 ||
       (head_dim != 64 && head_dim != 128))
     return 1;
   if (bh == 0 || sq == 0 || sk == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (head_dim == 128)
-    bf16_bwd_d<128>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, qks, sms, st);
+    bf16_bwd_d<128>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, qks, sms,
+                    split, st);
   else
-    bf16_bwd_d<64>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, qks, sms, st);
+    bf16_bwd_d<64>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, qks, sms,
+                   split, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_bf16_bwd_ex(const void* q, const void* k, const void* v, const void* dO_bf,
+                                 const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
+                                 void* dv, long bh, long sq, long sk, int group, int causal,
+                                 int head_dim, float qks, float sms, void* stream) {
+  return bf16_bwd_entry(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, head_dim,
+                        qks, sms, false, stream);
+}
+
+extern "C" int qattn_bf16_bwd_split_ex(const void* q, const void* k, const void* v, const void* dO_bf,
+                                       const void* LD, const void* q_bf, const void* k_bf, void* dq,
+                                       void* dk, void* dv, long bh, long sq, long sk, int group,
+                                       int causal, int head_dim, float qks, float sms, void* stream) {
+  return bf16_bwd_entry(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, head_dim,
+                        qks, sms, true, stream);
 }
 
 extern "C" int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf,

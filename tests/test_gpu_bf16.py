@@ -113,3 +113,25 @@ def test_bf16_gqa_fwd_bwd(lib, hq, hkv, sq, sk, causal):
     assert dk.shape == k.shape and dv.shape == v.shape and dq.shape == q.shape
     for name, a, b in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
         assert _rel(a.cpu(), b) <= 1e-2, (name, _rel(a.cpu(), b))
+
+
+@pytest.mark.parametrize("hq,hkv,sq,sk,d,causal", [
+    (2, 2, 256, 256, 128, False), (2, 2, 256, 256, 128, True), (4, 2, 160, 224, 128, False),
+    (4, 1, 96, 192, 128, True), (2, 2, 192, 320, 64, False), (3, 3, 128, 128, 64, True),
+    (2, 1, 1024, 1024, 128, True)])
+def test_bf16_bwd_fused_dkdv_bit_identical(lib, monkeypatch, hq, hkv, sq, sk, d, causal):
+    """The fused dK+dV kernel gives exactly the gradients of the separate dV and dK kernels
+    (same P / dS operands and accumulation order; partial workgroups, GQA, Sq != Sk, causal)."""
+    from quantizedattention_amd import attention_bf16 as A
+    g = torch.Generator().manual_seed(11)
+    q = torch.randn((1, hq, sq, d), generator=g).half().cuda()
+    k = torch.randn((1, hkv, sk, d), generator=g).half().cuda()
+    v = torch.randn((1, hkv, sk, d), generator=g).bfloat16().cuda()
+    dO = torch.randn((1, hq, sq, d), generator=g).cuda()
+    O, lse = A.helion_atten_bf16_fwd_training(q, k, v, causal)
+    fused = A.helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, causal, dO)
+    monkeypatch.setattr(A, "_BWD_ENTRY", "qattn_bf16_bwd_split_ex")
+    split = A.helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, causal, dO)
+    torch.cuda.synchronize()
+    for name, a, b in zip(("dq", "dk", "dv"), fused, split):
+        assert torch.equal(a, b), name
