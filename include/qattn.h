@@ -184,6 +184,18 @@ int qattn_bf16_bwd_ex(const void* q, const void* k, const void* v, const void* d
                       const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh, long sq,
                       long sk, int group, int causal, int head_dim, float qks, float sms, void* stream);
 
+/* Size in bytes of the dS record workspace of qattn_bf16_bwd_ws_ex: bh*(sq/32)*(sk/32)*2048
+ * (2 B per score), or -1 for sizes that are not multiples of 32. */
+long qattn_bf16_bwd_ws_bytes(long bh, long sq, long sk);
+
+/* qattn_bf16_bwd_ex whose fused dK+dV kernel also stores every bf16 dS tile in ws (device,
+ * qattn_bf16_bwd_ws_bytes bytes) and whose dQ pass reads them instead of recomputing S and dP:
+ * bit-identical dq, dk, dv. */
+int qattn_bf16_bwd_ws_ex(const void* q, const void* k, const void* v, const void* dO_bf,
+                         const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
+                         void* dv, long bh, long sq, long sk, int group, int causal, int head_dim,
+                         float qks, float sms, void* ws, void* stream);
+
 /* qattn_bf16_bwd_ex with separate dV and dK kernels (each recomputes S; two waves per SIMD each):
  * bit-identical dk, dv to the fused kernel; kept for the parity test and as a timing reference. */
 int qattn_bf16_bwd_split_ex(const void* q, const void* k, const void* v, const void* dO_bf,

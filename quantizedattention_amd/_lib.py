@@ -46,6 +46,9 @@ SIGNATURES = {
     "qattn_bf16_fwd_ex": [_vp] * 5 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
     "qattn_bf16_bwd_ex": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                         _c_float, _vp],
+    "qattn_bf16_bwd_ws_bytes": [_c_long, _c_long, _c_long],
+    "qattn_bf16_bwd_ws_ex": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
+                                           _c_float, _vp, _vp],
     "qattn_bf16_bwd_split_ex": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int,
                                               _c_float, _c_float, _vp],
     "qattn_bf16_bwd_prep": [_vp] * 5 + [_c_long, _c_long, _c_int, _vp],
@@ -71,7 +74,7 @@ SIGNATURES = {
 }
 
 # return types other than the int status code
-RESTYPES = {"qattn_int8_bwd_ws_bytes": ctypes.c_long}
+RESTYPES = {"qattn_int8_bwd_ws_bytes": ctypes.c_long, "qattn_bf16_bwd_ws_bytes": ctypes.c_long}
 
 _lib = None
 

@@ -15,6 +15,7 @@ attention, query head h reads key/value head h // (Hq / Hkv)); dk, dv then sum o
 from __future__ import annotations
 
 import math
+import os
 from typing import Tuple
 
 import torch
@@ -110,15 +111,30 @@ def helion_flash_atten_2_algo_4_bwd(
     dv = torch.empty((B, Hkv, Sk, D), dtype=torch.float32, device=dev)
     qks = _f32(1.0 / math.sqrt(D) * 1.44269504)
     sms = _f32(1.0 / math.sqrt(D))
-    _lib.call(_BWD_ENTRY, _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(LD),
-              _lib.ptr(q_bf), _lib.ptr(k_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
-              B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms, st)
+    args = (_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(LD), _lib.ptr(q_bf),
+            _lib.ptr(k_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
+            B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms)
+    ws = None
+    if _BWD_ENTRY == "ws":
+        ws_bytes = _lib.load().qattn_bf16_bwd_ws_bytes(B * H, S, Sk)
+        if 0 < ws_bytes <= WS_MAX_BYTES:
+            try:
+                ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
+            except torch.cuda.OutOfMemoryError:
+                ws = None   # no room for the dS records: recompute dS in the dQ pass (same results)
+    if ws is not None:
+        _lib.call("qattn_bf16_bwd_ws_ex", *args, _lib.ptr(ws), st)
+    else:
+        _lib.call("qattn_bf16_bwd_ex" if _BWD_ENTRY == "ws" else _BWD_ENTRY, *args, st)
     return dq, dk, dv
 
 
-# fused dK+dV kernel + dQ kernel; "qattn_bf16_bwd_split_ex" (separate dV and dK kernels, bit-identical
-# results) is the timing/parity reference
-_BWD_ENTRY = "qattn_bf16_bwd_ex"
+# "qattn_bf16_bwd_ex" (default): fused dK+dV, dQ recomputing S and dP; "ws" (QATTN_BF16_BWD_WS=1):
+# the fused kernel also stores bf16 dS records (2 B per score, up to QATTN_BWD_WS_MAX bytes) and dQ
+# reads them -- at config 3 the record traffic costs what the dQ pass saves;
+# "qattn_bf16_bwd_split_ex": separate dV and dK kernels.  All three give bit-identical gradients.
+_BWD_ENTRY = "ws" if os.environ.get("QATTN_BF16_BWD_WS") == "1" else "qattn_bf16_bwd_ex"
+WS_MAX_BYTES = int(os.environ.get("QATTN_BWD_WS_MAX", 16 << 30))
 
 
 class FlashAttention_2_BF16_autograd_function(Function):

@@ -83,6 +83,12 @@ enum B16Role { B16_DV = 0, B16_DK = 1, B16_DQ = 2, B16_DKV = 3 };
 #ifndef QA_B16_SCHED
 #define QA_B16_SCHED 0   // fused dK+dV: explicit MFMA / VALU interleave, bit 1 P wave, bit 2 dS wave
 #endif
+#ifndef QA_B16_WS_ST
+#define QA_B16_WS_ST 1   // dS record stores: 1 = 2 x b128 after a half-wave swap, 0 = 4 x b64, 2 = none (timing)
+#endif
+#ifndef QA_B16_DMA_P
+#define QA_B16_DMA_P 1   // fused dK+dV: only the P waves issue the ring DMA (dS waves never wait on vmcnt)
+#endif
 #ifndef QA_B16_DV_NSLOT
 #define QA_B16_DV_NSLOT 3
 #endif
@@ -107,7 +113,8 @@ struct B16Cfg {
   static constexpr int XROWS = 32 * 4;                      // own rows per workgroup
   static constexpr int NP = T16 / 1024;                     // 1-KiB LDS-DMA pieces per region
   static constexpr int INST = NREG * NP;
-  static constexpr int IPW16 = INST / WAVES;
+  static constexpr int DMA_WAVES = (FUSED && QA_B16_DMA_P) ? 4 : WAVES;   // waves issuing the DMA
+  static constexpr int IPW16 = INST / DMA_WAVES;
   static constexpr int IPW = IPW16 + (HAS_LD ? 1 : 0);      // VMEM ops per wave per tile
   static constexpr int NKS = D / 16;
   static constexpr int NDB = D / 32;
@@ -116,7 +123,7 @@ struct B16Cfg {
   static constexpr int PB_WAVE = 32 * 32 * 4, PB_TILE = 4 * PB_WAVE;
   static constexpr int RING = PBUF + (FUSED ? 2 * PB_TILE : 0);
   static constexpr int LDS = (RING > STAGE) ? RING : STAGE;
-  static_assert(INST % WAVES == 0, "DMA pieces split evenly over the waves");
+  static_assert(INST % DMA_WAVES == 0, "DMA pieces split evenly over the waves");
 };
 template <int D>
 QA_DEVICE int b16_rsw(int row) { return (D == 128) ? (row & 15) : ((row >> 1) & 7); }   // row reads
@@ -141,7 +148,7 @@ struct B16Dma {
     constexpr int RPI = 64 / G::NCH;
 #pragma unroll
     for (int i = 0; i < G::IPW16; ++i) {
-      const int p = wave + G::WAVES * i;
+      const int p = wave % G::DMA_WAVES + G::DMA_WAVES * i;
       const int r = p / G::NP, q = p % G::NP;
       const bool is_tr = r >= G::NROW;
       const int row = q * RPI + lane / G::NCH, c = lane % G::NCH;
@@ -151,9 +158,12 @@ struct B16Dma {
       rsrc[i] = make_rsrc(src[r], (unsigned)Sy * G::ROWB);
     }
     if constexpr (G::HAS_LD) ld_rsrc = make_rsrc(ld, (unsigned)Sy * 8);
-    ld_on = !G::FUSED || wave == G::WAVES - 1;   // FUSED: one wave brings the {lse, D} rows
+    ld_on = !G::FUSED || wave == G::DMA_WAVES - 1;   // FUSED: one wave brings the {lse, D} rows
+    dma_on = wave < G::DMA_WAVES;
   }
+  bool dma_on;
   QA_DEVICE void issue(unsigned slot_lds, int t, int lane) const {
+    if (!dma_on) return;
 #pragma unroll
     for (int i = 0; i < G::IPW16; ++i)
       dma16_buf(rsrc[i], voff[i], (unsigned)t * G::T16, slot_lds + lds_off[i]);
@@ -169,7 +179,7 @@ bf16_bwd_kernel(const _Float16* __restrict__ xa, const __bf16* __restrict__ xb,
                 const __bf16* __restrict__ ytr, const __bf16* __restrict__ ytr2,
                 const float2* __restrict__ yld, const float2* __restrict__ xld, float* __restrict__ out,
                 float* __restrict__ out2, int BH, int Sx, int Ny, int ydiv, int Smod, float qks,
-                float osc, float osc2) {
+                float osc, float osc2, __bf16* __restrict__ /*ws: fused kernel only*/) {
   using G = B16Cfg<D, ROLE>;
   constexpr bool TWO = G::TWO;
   static_assert(!G::FUSED, "B16_DKV runs bf16_bwd_dkv_kernel");
@@ -360,13 +370,16 @@ bf16_bwd_kernel(const _Float16* __restrict__ xa, const __bf16* __restrict__ xb,
 // carry 16 MFMAs per tile (S or dP, then dV or dK), S and P are computed once, and the P / dS
 // operands and accumulation order are those of the DV / DK kernels: dK, dV are bit-identical to
 // the split path.  Registers: one fragment set + one accumulator per wave, two waves per SIMD.
-template <int D, bool CAUSAL>
+// WS: the dS wave also stores each bf16 dS tile (exactly its dK operand) as a 2 KiB record, row-
+// major [key][query], at ((query head * Sq/32 + query tile) * Sk/32 + key tile) * 2 KiB, for
+// bf16_bwd_dqw_kernel.
+template <int D, bool CAUSAL, bool WS>
 __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
     const _Float16* __restrict__ xa, const __bf16* __restrict__ xb, const _Float16* __restrict__ ya,
     const __bf16* __restrict__ yb, const __bf16* __restrict__ ytr, const __bf16* __restrict__ ytr2,
     const float2* __restrict__ yld, const float2* __restrict__ xld, float* __restrict__ out,
     float* __restrict__ out2, int BH, int Sx, int Ny, int ydiv, int Smod, float qks, float osc,
-    float osc2) {
+    float osc2, __bf16* __restrict__ ws) {
   using G = B16Cfg<D, B16_DKV>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
@@ -439,7 +452,7 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
       op[s] = __builtin_bit_cast(v8bf, w);
     }
   };
-  auto accumulate = [&](auto SLc, const float* X) {
+  auto accumulate = [&](auto SLc, const v8bf* op) {
     const char* base = slot(SLc);
     v8bf ta[2 * G::NDB];
 #pragma unroll
@@ -448,8 +461,6 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
       for (int b = 0; b < G::NDB; ++b)
         ta[s * G::NDB + b] =
             __builtin_bit_cast(v8bf, ds_read_tr16_x2(base + troff[s][0][b], base + troff[s][1][b]));
-    v8bf op[2];
-    operand(X, op);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -460,8 +471,16 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   float X[16];
+  // an active dS wave of the WS kernel ends each step with its record stores, younger than the
+  // DMA of tile t+1: they may stay in flight across the barrier
+  const bool st_wave = WS && !pwave && active && QA_B16_WS_ST != 2;
   auto ring = [&](auto SLc, int t) {
-    ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();   // tile t+1 landed, P(t) written; slot t-1 free
+    static_assert(G::NSLOT == 3, "vmcnt counts below assume a 3-slot ring");
+    if (G::DMA_WAVES == 4 && !pwave) {
+      // no ring DMA in this wave: its record stores stay in flight
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (st_wave) ring_wait_barrier<QA_B16_WS_ST == 1 ? 2 : 4>();            // tile t+1 landed, P(t) written; slot t-1 free
+    else ring_wait_barrier<0>();
     dma.issue(smem_lds + ((decltype(SLc)::value + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
               min(t + G::NSLOT - 1, t1 - 1), lane);
   };
@@ -505,7 +524,9 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
     auto step = [&](auto SLc, auto NXc, int t) {
       ring(SLc, t);
       const v16f sa = sprod(NXc);
-      accumulate(SLc, X);                    // dV += dO^T P(t)
+      v8bf op[2];
+      operand(X, op);
+      accumulate(SLc, op);                   // dV += dO^T P(t)
       pvals(NXc, min(t + 1, t1 - 1), sa, pbuf(t + 1));
 #if QA_B16_SCHED & 1
       // LDS reads first, the 8 S MFMAs, then each dV MFMA followed by a share of the P VALU
@@ -557,8 +578,37 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) X[4 * g + j] = pv[g][j] * (pa[4 * g + j] - d_r[j]);
       }
-      accumulate(SLc, X);                    // dK += Q^T dS(t)
+      v8bf op[2];
+      operand(X, op);
+      accumulate(SLc, op);                   // dK += Q^T dS(t)
       pa = pn;
+      if constexpr (WS) {
+        // lane (key c32, half h) holds queries 8g + 4h + j of X[4g + j] (op[g/2], words 2(g%2)..+1)
+        if (active) {
+          char* r = reinterpret_cast<char*>(ws) +
+                    (((long)bh * (Ny / 32) + t) * (Sx / 32) + x0 / 32) * 2048 + c32 * 64;
+#if QA_B16_WS_ST == 1
+          // one permlane32_swap per word pair: the h=0 lane gets queries 0-15 of its key row, the
+          // h=1 lane queries 16-31; each writes 32 contiguous bytes (two b128 stores)
+          const v4u w0 = __builtin_bit_cast(v4u, op[0]), w1 = __builtin_bit_cast(v4u, op[1]);
+          v4u lo, hi;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const auto x = __builtin_amdgcn_permlane32_swap(w0[i], w1[i], false, false);
+            lo[i] = x[0];
+            hi[i] = x[1];
+          }
+          *reinterpret_cast<v4u*>(r + 32 * h) = v4u{lo[0], lo[1], hi[0], hi[1]};
+          *reinterpret_cast<v4u*>(r + 32 * h + 16) = v4u{lo[2], lo[3], hi[2], hi[3]};
+#elif QA_B16_WS_ST == 0
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const v4u w = __builtin_bit_cast(v4u, op[g >> 1]);
+            *reinterpret_cast<v2u*>(r + 16 * g + 8 * h) = v2u{w[2 * (g & 1)], w[2 * (g & 1) + 1]};
+          }
+#endif
+        }
+      }
 #if QA_B16_SCHED & 2
       // LDS reads first, then the dP MFMAs of tile t+1 each followed by a share of the dS(t) VALU
       __builtin_amdgcn_sched_group_barrier(0x100, 36, 0);
@@ -583,6 +633,132 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
   if (!active) return;
   store_rows<D, float, 2>(acc, pwave ? osc2 : osc, smem + wave * RowTile<D, float, 2>::BYTES,
                           (pwave ? out2 : out) + (hx + x0) * D, lane);
+}
+
+// ------------------------------------------------------------------- dQ from the dS records
+// dQ = sms * dS K without recomputing S, dP: 8 waves x 32 queries stream the bf16 k image (L2-
+// resident, 4-slot ring) and their own 2 KiB dS records (HBM, 5-slot ring, non-temporal).  A
+// record [key][query] read with ds_read_b64_tr_b16 is the dQ MFMA's B operand in the key order of
+// the k image read, i.e. exactly the operand the recomputing DQ kernel builds from its registers:
+// dq is bit-identical to it.  Causal: each wave visits the key tiles the recomputing kernel's
+// 128-query workgroup visits (floor(kt/4) <= floor(qt/4)), which are the tiles the fused dK+dV
+// kernel writes.
+template <int D>
+struct B16DqwCfg {
+  static constexpr int WAVES = 8;
+  static constexpr int ROWB = 2 * D;
+  static constexpr int T16 = 32 * ROWB;
+  static constexpr int NSLOT = 4, RSLOT = 5;
+  static constexpr int REC = WAVES * 2048;
+  static constexpr int RBASE = NSLOT * T16;
+  static constexpr int NP16 = T16 / 1024;
+  static constexpr int IPK = (NP16 + WAVES - 1) / WAVES;
+  static constexpr int NDB = D / 32;
+  static constexpr int RING = RBASE + RSLOT * REC;
+  static constexpr int STAGE = WAVES * RowTile<D, float, 2>::BYTES;
+  static constexpr int LDS = RING > STAGE ? RING : STAGE;
+};
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(512, 2) void bf16_bwd_dqw_kernel(const __bf16* __restrict__ ws,
+                                                              const __bf16* __restrict__ kbf,
+                                                              float* __restrict__ dq, int BH, int Sq,
+                                                              int Sk, int G, float sms) {
+  using W = B16DqwCfg<D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nqb = (Sq + 32 * W::WAVES - 1) / (32 * W::WAVES);
+  int bh, qb;
+  xcd_remap(blockIdx.x, nqb, BH, bh, qb);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int q0 = qb * 32 * W::WAVES + wave * 32;
+  const bool active = q0 < Sq;
+  const int nqt = Sq / 32, nkt = Sk / 32;
+  const long kv_row0 = (long)(bh / G) * Sk;
+  const int nt = CAUSAL ? min(nkt, 8 * qb + 8) : nkt;                      // workgroup's tiles
+  const int ntw = CAUSAL ? min(nkt, (q0 / 128) * 4 + 4) : nkt;             // this wave's tiles
+  const long rec0 = ((long)bh * nqt + (active ? q0 / 32 : 0)) * nkt;
+
+  unsigned kvoff[W::IPK], klds[W::IPK];
+  v4u krsrc[W::IPK];
+#pragma unroll
+  for (int i = 0; i < W::IPK; ++i) {
+    int pc = wave + W::WAVES * i;
+    if (pc >= W::NP16) pc = wave % W::NP16;
+    constexpr int NCH = W::ROWB / 16, RPI = 64 / NCH;
+    const int row = pc * RPI + lane / NCH, c = lane % NCH;
+    kvoff[i] = row * W::ROWB + 16 * (c ^ b16_tsw<D>(row));
+    klds[i] = pc * 1024;
+    krsrc[i] = make_rsrc(kbf + kv_row0 * D, (unsigned)Sk * W::ROWB);
+  }
+  const v4u rrsrc = make_rsrc(ws + rec0 * 1024, active ? (unsigned)nkt * 2048u : 0u);
+  const unsigned smem_lds = lds_addr(smem);
+  auto issue_k = [&](int t) {
+    const unsigned sl = smem_lds + (t % W::NSLOT) * W::T16;
+#pragma unroll
+    for (int i = 0; i < W::IPK; ++i)
+      dma16_buf(krsrc[i], kvoff[i], (unsigned)min(t, nt - 1) * W::T16, sl + klds[i]);
+  };
+  auto issue_r = [&](int t) {   // each record is read once: non-temporal
+    const unsigned sl = smem_lds + W::RBASE + (t % W::RSLOT) * W::REC + wave * 2048;
+    const unsigned so = (unsigned)min(t, nt - 1) * 2048u;
+    dma16_buf_nt(rrsrc, 16u * lane, so, sl);
+    dma16_buf_nt(rrsrc, 16u * lane, so + 1024u, sl + 1024u);
+  };
+  if (nt > 0) {
+#pragma unroll
+    for (int i = 0; i < W::NSLOT - 1; ++i) issue_k(i);
+    for (int i = 0; i < W::RSLOT - 1; ++i) issue_r(i);
+  }
+  int troff[W::NDB];
+  int rtro;
+  {
+    const int gg = (lane >> 4) & 1, i16 = lane & 15;
+    const int row = 4 * h + (i16 >> 2);
+#pragma unroll
+    for (int b = 0; b < W::NDB; ++b) {
+      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
+      troff[b] = row * W::ROWB + 16 * ((d / 8) ^ b16_tsw<D>(row)) + (d % 8) * 2;
+    }
+    rtro = row * 64 + 2 * (16 * gg + 4 * (i16 & 3));
+  }
+  v16f acc[W::NDB];
+#pragma unroll
+  for (int b = 0; b < W::NDB; ++b) acc[b] = v16f{};
+
+  vmem_drain();
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    // tile t's k image landed (and its record, issued earlier): younger than the k DMA of tile t
+    // are the 2 record DMAs issued with it and the k + record DMAs of the two iterations since
+    ring_wait_barrier<2 + (W::NSLOT - 2) * (W::IPK + 2)>();
+    issue_k(t + W::NSLOT - 1);
+    issue_r(t + W::RSLOT - 1);
+    if (active && t < ntw) {
+      const char* kb = smem + (t % W::NSLOT) * W::T16;
+      const char* rb = smem + W::RBASE + (t % W::RSLOT) * W::REC + wave * 2048 + rtro;
+      v8bf ta[2 * W::NDB], op[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int b = 0; b < W::NDB; ++b) {
+          const char* a = kb + troff[b] + 16 * s * W::ROWB;
+          ta[s * W::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * W::ROWB));
+        }
+        op[s] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(rb + 16 * s * 64, rb + 16 * s * 64 + 8 * 64));
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int b = 0; b < W::NDB; ++b) acc[b] = mfma_bf16(ta[s * W::NDB + b], op[s], acc[b]);
+    }
+  }
+  vmcnt_wait_all();
+  __syncthreads();   // the rings become the output staging area
+  if (!active) return;
+  store_rows<D, float, 2>(acc, sms, smem + wave * RowTile<D, float, 2>::BYTES,
+                          dq + ((long)bh * Sq + q0) * D, lane);
 }
 
 }  // namespace qattn
@@ -620,13 +796,13 @@ struct B16Out {
   void* out2;
   float osc, osc2;
 };
-template <int D, int ROLE, bool CAUSAL>
+template <int D, int ROLE, bool CAUSAL, bool WS>
 static void launch_b16c(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
                         const void* ytr2, const void* yld, const void* xld, B16Out o, long bh, long sx,
-                        long ny, int ydiv, long smod, float qks, hipStream_t st) {
+                        long ny, int ydiv, long smod, float qks, void* ws, hipStream_t st) {
   using G = B16Cfg<D, ROLE>;
   auto kern = [] {
-    if constexpr (ROLE == B16_DKV) return bf16_bwd_dkv_kernel<D, CAUSAL>;
+    if constexpr (ROLE == B16_DKV) return bf16_bwd_dkv_kernel<D, CAUSAL, WS>;
     else return bf16_bwd_kernel<D, ROLE, CAUSAL>;
   }();
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
@@ -635,16 +811,32 @@ static void launch_b16c(const void* xa, const void* xb, const void* ya, const vo
                      G::LDS, st, (const _Float16*)xa, (const __bf16*)xb, (const _Float16*)ya,
                      (const __bf16*)yb, (const __bf16*)ytr, (const __bf16*)ytr2, (const float2*)yld,
                      (const float2*)xld, (float*)o.out, (float*)o.out2, (int)bh, (int)sx, (int)ny,
-                     ydiv, (int)smod, qks, o.osc, o.osc2);
+                     ydiv, (int)smod, qks, o.osc, o.osc2, (__bf16*)ws);
 }
 template <int D, int ROLE>
 static void launch_b16(const void* xa, const void* xb, const void* ya, const void* yb, const void* ytr,
                        const void* ytr2, const void* yld, const void* xld, B16Out o, long bh, long sx,
-                       long ny, int ydiv, long smod, int causal, float qks, hipStream_t st) {
-  if (causal)
-    launch_b16c<D, ROLE, true>(xa, xb, ya, yb, ytr, ytr2, yld, xld, o, bh, sx, ny, ydiv, smod, qks, st);
-  else
-    launch_b16c<D, ROLE, false>(xa, xb, ya, yb, ytr, ytr2, yld, xld, o, bh, sx, ny, ydiv, smod, qks, st);
+                       long ny, int ydiv, long smod, int causal, float qks, hipStream_t st,
+                       void* ws = nullptr) {
+#define QA_L(C, W) launch_b16c<D, ROLE, C, W>(xa, xb, ya, yb, ytr, ytr2, yld, xld, o, bh, sx, ny, ydiv, \
+                                              smod, qks, ws, st)
+  if (ROLE == B16_DKV && ws) {
+    if (causal) QA_L(true, true); else QA_L(false, true);
+  } else {
+    if (causal) QA_L(true, false); else QA_L(false, false);
+  }
+#undef QA_L
+}
+template <int D, bool CAUSAL>
+static void launch_dqw_b16c(const void* ws, const void* k_bf, void* dq, long bh, long sq, long sk,
+                            int group, float sms, hipStream_t st) {
+  using W = B16DqwCfg<D>;
+  hipFuncSetAttribute((const void*)bf16_bwd_dqw_kernel<D, CAUSAL>,
+                      hipFuncAttributeMaxDynamicSharedMemorySize, W::LDS);
+  const int nb = (int)((sq + 32 * W::WAVES - 1) / (32 * W::WAVES));
+  hipLaunchKernelGGL((bf16_bwd_dqw_kernel<D, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * W::WAVES),
+                     W::LDS, st, (const __bf16*)ws, (const __bf16*)k_bf, (float*)dq, (int)bh, (int)sq,
+                     (int)sk, group, sms);
 }
 
 // bh = batch * query heads; key/value tensors have bh / group heads of sk rows
@@ -652,8 +844,16 @@ template <int D>
 static void bf16_bwd_d(const void* q, const void* k, const void* v, const void* dO_bf, const void* LD,
                        const void* q_bf, const void* k_bf, void* dq, void* dk, void* dv, long bh,
                        long sq, long sk, int group, int causal, float qks, float sms, bool split,
-                       hipStream_t st) {
+                       void* ws, hipStream_t st) {
   const long bkv = bh / group, ny = group * sq;
+  if (ws) {
+    // dK + dV storing the dS records, then dQ from the records
+    launch_b16<D, B16_DKV>(k, v, q, dO_bf, q_bf, dO_bf, LD, nullptr, {dk, dv, sms, 1.0f}, bkv, sk, ny, 1,
+                           sq, causal, qks, st, ws);
+    if (causal) launch_dqw_b16c<D, true>(ws, k_bf, dq, bh, sq, sk, group, sms, st);
+    else launch_dqw_b16c<D, false>(ws, k_bf, dq, bh, sq, sk, group, sms, st);
+    return;
+  }
   if (split) {
     // dV: own K / streamed Q rows, dO tr image, LD
     launch_b16<D, B16_DV>(k, nullptr, q, nullptr, dO_bf, nullptr, LD, nullptr, {dv, nullptr, 1.0f, 0.f},
@@ -674,7 +874,7 @@ static void bf16_bwd_d(const void* q, const void* k, const void* v, const void* 
 static int bf16_bwd_entry(const void* q, const void* k, const void* v, const void* dO_bf,
                           const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
                           void* dv, long bh, long sq, long sk, int group, int causal, int head_dim,
-                          float qks, float sms, bool split, void* stream) {
+                          float qks, float sms, bool split, void* ws, void* stream) {
   if (sq % 32 != 0 || sk % 32 != 0 || group < 1 || bh % group != 0 ||
       (head_dim != 64 && head_dim != 128))
     return 1;
@@ -682,10 +882,10 @@ static int bf16_bwd_entry(const void* q, const void* k, const void* v, const voi
   hipStream_t st = (hipStream_t)stream;
   if (head_dim == 128)
     bf16_bwd_d<128>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, qks, sms,
-                    split, st);
+                    split, ws, st);
   else
     bf16_bwd_d<64>(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, qks, sms,
-                   split, st);
+                   split, ws, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -694,7 +894,22 @@ extern "C" int qattn_bf16_bwd_ex(const void* q, const void* k, const void* v, co
                                  void* dv, long bh, long sq, long sk, int group, int causal,
                                  int head_dim, float qks, float sms, void* stream) {
   return bf16_bwd_entry(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, head_dim,
-                        qks, sms, false, stream);
+                        qks, sms, false, nullptr, stream);
+}
+
+// bytes of the dS record workspace of qattn_bf16_bwd_ws_ex (-1 on invalid sizes)
+extern "C" long qattn_bf16_bwd_ws_bytes(long bh, long sq, long sk) {
+  if (bh < 0 || sq < 0 || sk < 0 || sq % 32 != 0 || sk % 32 != 0) return -1;
+  return bh * (sq / 32) * (sk / 32) * 2048;
+}
+
+extern "C" int qattn_bf16_bwd_ws_ex(const void* q, const void* k, const void* v, const void* dO_bf,
+                                    const void* LD, const void* q_bf, const void* k_bf, void* dq, void* dk,
+                                    void* dv, long bh, long sq, long sk, int group, int causal,
+                                    int head_dim, float qks, float sms, void* ws, void* stream) {
+  if (!ws) return 1;
+  return bf16_bwd_entry(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, head_dim,
+                        qks, sms, false, ws, stream);
 }
 
 extern "C" int qattn_bf16_bwd_split_ex(const void* q, const void* k, const void* v, const void* dO_bf,
@@ -702,7 +917,7 @@ extern "C" int qattn_bf16_bwd_split_ex(const void* q, const void* k, const void*
                                        void* dk, void* dv, long bh, long sq, long sk, int group,
                                        int causal, int head_dim, float qks, float sms, void* stream) {
   return bf16_bwd_entry(q, k, v, dO_bf, LD, q_bf, k_bf, dq, dk, dv, bh, sq, sk, group, causal, head_dim,
-                        qks, sms, true, stream);
+                        qks, sms, true, nullptr, stream);
 }
 
 extern "C" int qattn_bf16_bwd(const void* q, const void* k, const void* v, const void* dO_bf,

@@ -145,3 +145,6 @@ def test_bwd_workspace_size():
     assert lib.qattn_int8_bwd_ws_bytes(6, 96, 160) == 6 * 3 * 5 * 1028
     assert lib.qattn_int8_bwd_ws_bytes(2, 100, 64) == -1          # tokens not a multiple of 32
     assert lib.qattn_int8_bwd_ws_bytes(0, 64, 64) == 0
+    assert lib.qattn_bf16_bwd_ws_bytes(4 * 32, 4096, 4096) == 128 * 128 * 128 * 2048
+    assert lib.qattn_bf16_bwd_ws_bytes(6, 96, 160) == 6 * 3 * 5 * 2048
+    assert lib.qattn_bf16_bwd_ws_bytes(2, 100, 64) == -1

@@ -120,8 +120,9 @@ def test_bf16_gqa_fwd_bwd(lib, hq, hkv, sq, sk, causal):
     (4, 1, 96, 192, 128, True), (2, 2, 192, 320, 64, False), (3, 3, 128, 128, 64, True),
     (2, 1, 1024, 1024, 128, True)])
 def test_bf16_bwd_fused_dkdv_bit_identical(lib, monkeypatch, hq, hkv, sq, sk, d, causal):
-    """The fused dK+dV kernel gives exactly the gradients of the separate dV and dK kernels
-    (same P / dS operands and accumulation order; partial workgroups, GQA, Sq != Sk, causal)."""
+    """The fused dK+dV path (default: dQ recomputes dS), its dS-record variant (dQ reads bf16 dS
+    records) and the split dV / dK kernels give identical gradients (same P / dS operands and
+    accumulation order; partial workgroups, GQA, Sq != Sk, causal)."""
     from quantizedattention_amd import attention_bf16 as A
     g = torch.Generator().manual_seed(11)
     q = torch.randn((1, hq, sq, d), generator=g).half().cuda()
@@ -129,9 +130,13 @@ def test_bf16_bwd_fused_dkdv_bit_identical(lib, monkeypatch, hq, hkv, sq, sk, d,
     v = torch.randn((1, hkv, sk, d), generator=g).bfloat16().cuda()
     dO = torch.randn((1, hq, sq, d), generator=g).cuda()
     O, lse = A.helion_atten_bf16_fwd_training(q, k, v, causal)
+    monkeypatch.setattr(A, "_BWD_ENTRY", "ws")
+    ws = A.helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, causal, dO)
+    monkeypatch.setattr(A, "_BWD_ENTRY", "qattn_bf16_bwd_ex")
     fused = A.helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, causal, dO)
     monkeypatch.setattr(A, "_BWD_ENTRY", "qattn_bf16_bwd_split_ex")
     split = A.helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, causal, dO)
     torch.cuda.synchronize()
-    for name, a, b in zip(("dq", "dk", "dv"), fused, split):
+    for name, a, b, c in zip(("dq", "dk", "dv"), ws, fused, split):
         assert torch.equal(a, b), name
+        assert torch.equal(b, c), name

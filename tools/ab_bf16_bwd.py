@@ -1,4 +1,4 @@
-"""Time the bf16 backward at config 3: fused dK+dV (default) and split dV/dK (dev A/B tool).
+"""Time the bf16 backward at config 3: dS records (default), fused dK+dV, split dV/dK (dev A/B).
 
     python3 tools/ab_bf16_bwd.py [B,H,S,D] [causal]
 Prints the median event time of each backward call; also usable under rocprofv3 --kernel-trace.
@@ -20,7 +20,7 @@ v = torch.randn((B, H, S, D), device="cuda", generator=g).bfloat16()
 dO = torch.randn((B, H, S, D), device="cuda", generator=g)
 O, lse = A.helion_atten_bf16_fwd_training(q, k, v, causal)
 res = {}
-for entry in ("qattn_bf16_bwd_ex", "qattn_bf16_bwd_split_ex"):
+for entry in ("ws", "qattn_bf16_bwd_ex", "qattn_bf16_bwd_split_ex"):
     A._BWD_ENTRY = entry
     ts = []
     for i in range(8):
