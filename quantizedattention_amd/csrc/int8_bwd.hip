@@ -640,7 +640,11 @@ struct DqwCfg {
   static constexpr int WAVES = QA_DQW_WAVES;
   static constexpr int T16 = 64 * D;               // bf16 k image of a 32-key tile (L2-resident)
   static constexpr int NSLOT = 4;                  // k image ring: 3 tiles ahead
+#ifdef QA_DQW_RSLOT
+  static constexpr int RSLOT = QA_DQW_RSLOT;
+#else
   static constexpr int RSLOT = WAVES >= 16 ? 4 : WAVES == 8 ? 5 : 10;   // record ring (HBM stream)
+#endif
   static constexpr int REC = WAVES * 1024;         // the waves' dS records of one tile
   static constexpr int RBASE = NSLOT * T16;
   static constexpr int NP16 = T16 / 1024;

@@ -8,6 +8,7 @@ implementation giving output shapes and dtypes without running anything; ``int8_
 ``bf16_fwd`` carry autograd rules (their backward operators), so compiled training steps
 differentiate through them.
 
+    torch.ops.qattn.int8_quant(x, block) -> (idx, scale)
     torch.ops.qattn.int8_fwd(q, k, v, smooth, causal) -> (O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
     torch.ops.qattn.int8_bwd(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, causal, kv_heads)
         -> (dq, dk, dv)
@@ -33,12 +34,37 @@ from . import attention_int8 as _i8
 from . import attention_jvp as _jvp
 from . import attention_mxfp4 as _fp4
 
-__all__ = ["int8_fwd", "int8_bwd", "bf16_fwd", "bf16_bwd", "jvp_fwd", "mxfp4_fwd"]
+__all__ = ["int8_quant", "int8_fwd", "int8_bwd", "bf16_fwd", "bf16_bwd", "jvp_fwd", "mxfp4_fwd"]
 
 _LIB = "qattn"
 
 
 # ------------------------------------------------------------------------------------ int8
+@torch.library.custom_op(f"{_LIB}::int8_quant", mutates_args=(), device_types="cuda")
+def int8_quant(x: Tensor, block: int) -> Tuple[Tensor, Tensor]:
+    """Per-32-token block quantiser (attention_int8.py:178-186): x fp16 [..., S, D] ->
+    (idx int8 [..., S, D], scale fp16 [..., S/32]); s = f16(amax/127), idx = trunc(f16(x/s))."""
+    if block != 32:
+        raise ValueError("qattn::int8_quant supports block = 32 (the reference's Bq = Bkv)")
+    if x.dim() < 2 or x.shape[-2] % 32 != 0 or x.shape[-1] not in (64, 128):
+        raise ValueError("qattn::int8_quant needs x [..., S, D] with S % 32 == 0 and D in (64, 128)")
+    from . import _lib
+    _lib.require_gpu(x)
+    xh = x.to(torch.float16).contiguous()
+    rows, D = xh.numel() // x.shape[-1], x.shape[-1]
+    idx = torch.empty(xh.shape, dtype=torch.int8, device=x.device)
+    scale = torch.empty((*xh.shape[:-2], xh.shape[-2] // 32), dtype=torch.float16, device=x.device)
+    _lib.call("qattn_int8_quant", _lib.ptr(xh), _lib.ptr(idx), _lib.ptr(scale), None, None, rows,
+              xh.shape[-2], D, _lib.stream_of(xh))
+    return idx, scale
+
+
+@int8_quant.register_fake
+def _(x, block):
+    return (x.new_empty(x.shape, dtype=torch.int8),
+            x.new_empty((*x.shape[:-2], x.shape[-2] // 32), dtype=torch.float16))
+
+
 @torch.library.custom_op(f"{_LIB}::int8_fwd", mutates_args=(), device_types="cuda")
 def int8_fwd(q: Tensor, k: Tensor, v: Tensor, smooth: bool, causal: bool
              ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:

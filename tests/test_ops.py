@@ -9,7 +9,7 @@ import quantizedattention_amd.ops  # noqa: F401  (registers torch.ops.qattn.*)
 
 
 def test_ops_registered():
-    for name in ("int8_fwd", "int8_bwd", "bf16_fwd", "bf16_bwd", "jvp_fwd", "mxfp4_fwd"):
+    for name in ("int8_quant", "int8_fwd", "int8_bwd", "bf16_fwd", "bf16_bwd", "jvp_fwd", "mxfp4_fwd"):
         assert hasattr(torch.ops.qattn, name), name
 
 
@@ -30,6 +30,8 @@ def test_fake_shapes():
         Oj, tOj, lj = torch.ops.qattn.jvp_fwd(q, k, k, q, k, k)
         assert tOj.shape == q.shape and lj.shape == (16, 256)
         assert torch.ops.qattn.mxfp4_fwd(q, k, k).shape == q.shape
+        idx, sc = torch.ops.qattn.int8_quant(k, 32)
+        assert idx.shape == k.shape and idx.dtype == torch.int8 and sc.shape == (2, 2, 16)
     assert mode is not None
 
 
@@ -76,3 +78,18 @@ def test_ops_autograd_matches_dropins(lib):
     flash_atten_2_bf16(*b, False).backward(dO.float())
     for x, y in zip(a, b):
         assert torch.equal(x.grad, y.grad)
+
+
+@pytest.mark.gpu
+def test_int8_quant_op_bit_exact(lib):
+    """qattn::int8_quant equals the oracle's restatement of the reference quantiser bit for bit
+    (including an all-zero block)."""
+    from oracle import restate as R
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn((2, 3, 128, 128), generator=g) * 4).half()
+    x[0, 1, 32:64] = 0
+    idx, sc = torch.ops.qattn.int8_quant(x.cuda(), 32)
+    ridx, rsc = R.quant_blocks(x)
+    assert torch.equal(idx.cpu(), ridx) and torch.equal(sc.cpu(), rsc)
+    with pytest.raises(ValueError):
+        torch.ops.qattn.int8_quant(x.cuda(), 64)
