@@ -299,6 +299,9 @@ void int8_bwd_kernel(
   const long yrow = (long)(bh / ydiv) * Ny;        // streamed rows
   // causal dQ: key tiles past the workgroup's last query are masked for all of its rows
   const int nt = (CAUSAL && ROLE == ROLE_DQ) ? min(Ny / 32, (xt * G::XROWS + G::XROWS) / 32) : Ny / 32;
+  // causal dK/dV: query tiles before the workgroup's first key are masked for all of its rows
+  // (P = 0 exactly, so skipping them is exact); tiles t0 .. nt-1 are visited
+  const int t0 = (CAUSAL && ROLE != ROLE_DQ && Ny == Smod) ? min(nt, (xt * G::XROWS) / 32) : 0;
 
   BwdDma<D, ROLE> dma;
   dma.init(wave, lane, Ny, reinterpret_cast<const char*>(y8a + yrow * D),
@@ -306,7 +309,8 @@ void int8_bwd_kernel(
            reinterpret_cast<const char*>(ytr2 + yrow * D), reinterpret_cast<const char*>(yld + yrow));
   const unsigned smem_lds = lds_addr(smem);
 #pragma unroll
-  for (int i = 0; i < G::NSLOT - 1; ++i) dma.issue(smem_lds + i * G::SLOT, min(i, nt - 1), lane);
+  for (int i = 0; i < G::NSLOT - 1; ++i)
+    dma.issue(smem_lds + ((t0 + i) % G::NSLOT) * G::SLOT, min(t0 + i, nt - 1), lane);
   // per-tile scales of the streamed side, once, in LDS (a global load inside the loop would make
   // hipcc wait vmcnt for the in-flight LDS-DMA)
   _Float16* sc_lds = reinterpret_cast<_Float16*>(smem + G::NSLOT * G::SLOT);
@@ -506,12 +510,12 @@ void int8_bwd_kernel(
   __syncthreads();
   if constexpr (G::PIPE) {
     float X[16];
-    if (active) {
+    if (active && t0 < nt) {
       v16i sa, pa;
-      products(0, sa, pa);
-      values(0, sa, pa, X, X);
+      products(t0, sa, pa);
+      values(t0, sa, pa, X, X);
     }
-    for (int t = 0; t < nt; ++t) {
+    for (int t = t0; t < nt; ++t) {
       // tile t+1 landed (later tiles may be in flight); the slot of tile t-1 is free
       ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
       dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
@@ -533,18 +537,18 @@ void int8_bwd_kernel(
     // int8 products for tile t+1 are issued first and whose fp32 values of t+1 are computed beside
     // the bf16 MFMAs of tile t
     v8bf opS[2], opP[2];
-    if (active) {
+    if (active && t0 < nt) {
       v16i sa, pa;
-      products(0, sa, pa);
+      products(t0, sa, pa);
       float P[16], dS[16];
-      values(0, sa, pa, P, dS);
-      quantise_ds(dS, 0, opS);
-      quantise(P, so_p(0), opP);
+      values(t0, sa, pa, P, dS);
+      quantise_ds(dS, t0, opS);
+      quantise(P, so_p(t0), opP);
     }
 #if QA_DKV_PRIO
     __builtin_amdgcn_s_setprio(1);
 #endif
-    for (int t = 0; t < nt; ++t) {
+    for (int t = t0; t < nt; ++t) {
       // tile t+1 landed: younger than its DMA are the workspace stores of tile t-1, the DMA of
       // tile t+2 and the stores of tile t
       if (active) ring_wait_barrier<(G::NSLOT - 3) * G::IPW + 2 * WS_OPS>();
@@ -567,7 +571,7 @@ void int8_bwd_kernel(
       }
     }
   } else {
-    for (int t = 0; t < nt; ++t) {
+    for (int t = t0; t < nt; ++t) {
       // tile t landed (t+1, t+2 may be in flight); the slot of tile t-1 is free.  With the stagger
       // the other half of the workgroup reads tile t+1 after this barrier: wait for it too.
       // (the workspace stores of an active wave, WS_OPS per tile, sit between the DMAs)
@@ -598,7 +602,7 @@ void int8_bwd_kernel(
   if (!active) return;
   if constexpr (WS) {   // this wave's s_dS column: record (t, x0/32) of the key/value head
     const int nkt = Sx / 32;
-    for (int t = lane; t < nt; t += 64) sds[ws_first + (long)t * nkt + x0 / 32] = sds_lds[wave * nt + t];
+    for (int t = t0 + lane; t < nt; t += 64) sds[ws_first + (long)t * nkt + x0 / 32] = sds_lds[wave * nt + t];
   }
   const long r = hrow + x0 + c32;
   auto store = [&](const v16f* ac, float osc, _Float16* dst) {
