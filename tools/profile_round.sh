@@ -22,3 +22,6 @@ echo "write done"
 timeout -k 10 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES --output-format csv \
   -d $OUT/mfma -o run -- python3 $R/tools/kernel_runner.py int8_all 2 > /dev/null 2>&1
 echo "mfma done"
+timeout -k 10 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_I8 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+  --output-format csv -d $OUT/mops -o run -- python3 $R/tools/kernel_runner.py int8_all 2 > /dev/null 2>&1
+echo "mops done"

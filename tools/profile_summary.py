@@ -79,6 +79,7 @@ def main():
     fetch = counters(os.path.join(src, "fetch"))
     write = counters(os.path.join(src, "write"))
     mfma = counters(os.path.join(src, "mfma"))
+    mops = counters(os.path.join(src, "mops")) if os.path.isdir(os.path.join(src, "mops")) else {}
     out, traffic = {}, {}
     for k in KEYS:
         e = {}
@@ -93,6 +94,12 @@ def main():
             cyc = m["GRBM_GUI_ACTIVE"] / XCDS
             e["mfma_util"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS_PER_XCD * XCDS)
             e["gpu_cycles"] = cyc
+        if k in mops:
+            # MFMA work the kernel executed (512 ops per MOPS unit), against what bench credits it
+            m = mops[k]
+            e.update(m)
+            e["mfma_ops_executed"] = 512 * sum(m.get(c, 0.0) for c in (
+                "SQ_INSTS_VALU_MFMA_MOPS_I8", "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_INSTS_VALU_MFMA_MOPS_BF16"))
         if "FETCH_bytes_x2" in e and "WRITE_bytes" in e:
             traffic[k] = e["FETCH_bytes_x2"] + e["WRITE_bytes"]
             e["hbm_bytes_per_launch"] = traffic[k]
