@@ -114,8 +114,11 @@ def helion_flash_atten_2_algo_4_bwd(
     args = (_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(dO_bf), _lib.ptr(LD), _lib.ptr(q_bf),
             _lib.ptr(k_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv),
             B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms)
+    entry = _BWD_ENTRY
+    if entry == "auto":
+        entry = "ws" if causal else "qattn_bf16_bwd_ex"
     ws = None
-    if _BWD_ENTRY == "ws":
+    if entry == "ws":
         ws_bytes = _lib.load().qattn_bf16_bwd_ws_bytes(B * H, S, Sk)
         if 0 < ws_bytes <= WS_MAX_BYTES:
             try:
@@ -125,15 +128,16 @@ def helion_flash_atten_2_algo_4_bwd(
     if ws is not None:
         _lib.call("qattn_bf16_bwd_ws_ex", *args, _lib.ptr(ws), st)
     else:
-        _lib.call("qattn_bf16_bwd_ex" if _BWD_ENTRY == "ws" else _BWD_ENTRY, *args, st)
+        _lib.call("qattn_bf16_bwd_ex" if entry == "ws" else entry, *args, st)
     return dq, dk, dv
 
 
-# "qattn_bf16_bwd_ex" (default): fused dK+dV, dQ recomputing S and dP; "ws" (QATTN_BF16_BWD_WS=1):
-# the fused kernel also stores bf16 dS records (2 B per score, up to QATTN_BWD_WS_MAX bytes) and dQ
-# reads them -- at config 3 the record traffic costs what the dQ pass saves;
-# "qattn_bf16_bwd_split_ex": separate dV and dK kernels.  All three give bit-identical gradients.
-_BWD_ENTRY = "ws" if os.environ.get("QATTN_BF16_BWD_WS") == "1" else "qattn_bf16_bwd_ex"
+# "auto" (default): causal -> "ws", else "qattn_bf16_bwd_ex".  "qattn_bf16_bwd_ex": fused dK+dV, dQ
+# recomputing S and dP; "ws": the fused kernel also stores bf16 dS records (2 B per score, up to
+# QATTN_BWD_WS_MAX bytes) and dQ reads them -- non-causal at config 3 the record traffic costs what
+# the dQ pass saves, causal it is 7 % faster; "qattn_bf16_bwd_split_ex": separate dV
+# and dK kernels.  All give bit-identical gradients.  QATTN_BF16_BWD_WS=1 / 0 forces ws on / off.
+_BWD_ENTRY = {"1": "ws", "0": "qattn_bf16_bwd_ex"}.get(os.environ.get("QATTN_BF16_BWD_WS", ""), "auto")
 WS_MAX_BYTES = int(os.environ.get("QATTN_BWD_WS_MAX", 16 << 30))
 
 

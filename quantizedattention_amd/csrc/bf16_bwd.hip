@@ -89,6 +89,9 @@ enum B16Role { B16_DV = 0, B16_DK = 1, B16_DQ = 2, B16_DKV = 3 };
 #ifndef QA_B16_DMA_P
 #define QA_B16_DMA_P 1   // fused dK+dV: only the P waves issue the ring DMA (dS waves never wait on vmcnt)
 #endif
+#ifndef QA_B16_DQ_WAVES
+#define QA_B16_DQ_WAVES 8   // dQ workgroup: 4 or 8 waves of 32 queries (8 halves the k/v stream per query)
+#endif
 #ifndef QA_B16_DV_NSLOT
 #define QA_B16_DV_NSLOT 3
 #endif
@@ -109,8 +112,8 @@ struct B16Cfg {
   static constexpr int YA = 0, YB = T16, TR = NROW * T16, TR2 = MERGE ? YB : 3 * T16, LDO = NREG * T16;
   static constexpr int SLOT = NREG * T16 + (HAS_LD ? 256 : 0);
   static constexpr int NSLOT = (ROLE == B16_DV) ? QA_B16_DV_NSLOT : 3;
-  static constexpr int WAVES = FUSED ? 8 : 4;
-  static constexpr int XROWS = 32 * 4;                      // own rows per workgroup
+  static constexpr int WAVES = FUSED ? 8 : (ROLE == B16_DQ && D == 128) ? QA_B16_DQ_WAVES : 4;
+  static constexpr int XROWS = 32 * (FUSED ? 4 : WAVES);    // own rows per workgroup
   static constexpr int NP = T16 / 1024;                     // 1-KiB LDS-DMA pieces per region
   static constexpr int INST = NREG * NP;
   static constexpr int DMA_WAVES = (FUSED && QA_B16_DMA_P) ? 4 : WAVES;   // waves issuing the DMA
@@ -173,7 +176,7 @@ struct B16Dma {
 };
 
 template <int D, int ROLE, bool CAUSAL>
-__global__ __launch_bounds__(256, ROLE == B16_DV ? QA_B16_DV_OCC : 2) void
+__global__ __launch_bounds__((64 * B16Cfg<D, ROLE>::WAVES), ROLE == B16_DV ? QA_B16_DV_OCC : 2) void
 bf16_bwd_kernel(const _Float16* __restrict__ xa, const __bf16* __restrict__ xb,
                 const _Float16* __restrict__ ya, const __bf16* __restrict__ yb,
                 const __bf16* __restrict__ ytr, const __bf16* __restrict__ ytr2,
@@ -205,6 +208,9 @@ bf16_bwd_kernel(const _Float16* __restrict__ xa, const __bf16* __restrict__ xb,
     else if (Ny == Smod) t0 = min(t1, (xt * G::XROWS) / 32);              // queries <= every key
   }
   const int nt = t1 - t0;
+  // causal dQ accumulates, per wave, the key tiles of its 128-query block (floor(kt/4) <=
+  // floor(qt/4)) whatever the workgroup size: the same tiles as the dK+dV kernel's records cover
+  const int t1w = (CAUSAL && ROLE == B16_DQ) ? min(t1, (x0 / 128) * 4 + 4) : t1;
 
   B16Dma<D, ROLE> dma;
   {
@@ -337,10 +343,12 @@ bf16_bwd_kernel(const _Float16* __restrict__ xa, const __bf16* __restrict__ xb,
     products(NXc, sa, pa);
     v8bf op[2];
     operand(X, op);
+    if (t < t1w) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int b = 0; b < G::NDB; ++b) acc[b] = mfma_bf16(ta[s * G::NDB + b], op[s], acc[b]);
+        for (int b = 0; b < G::NDB; ++b) acc[b] = mfma_bf16(ta[s * G::NDB + b], op[s], acc[b]);
+    }
     values(NXc, tn, sa, pa, X);
   };
   if (nt > 0) {

@@ -20,7 +20,7 @@ v = torch.randn((B, H, S, D), device="cuda", generator=g).bfloat16()
 dO = torch.randn((B, H, S, D), device="cuda", generator=g)
 O, lse = A.helion_atten_bf16_fwd_training(q, k, v, causal)
 res = {}
-for entry in ("ws", "qattn_bf16_bwd_ex", "qattn_bf16_bwd_split_ex"):
+for entry in ("auto", "ws", "qattn_bf16_bwd_ex", "qattn_bf16_bwd_split_ex"):
     A._BWD_ENTRY = entry
     ts = []
     for i in range(8):
