@@ -172,7 +172,8 @@ def mxfp4_fwd_times(q, k, v, n):
 def other_configs(n):
     """BASELINE.json's other GPU configs, each timed alone on this rank (HIP events, ms per call):
     config 2, bf16 fwd+bwd (4,32,2048,128); config 5, the JVP forward (2,16,2048,128) with bf16
-    inputs and randn tangents.  (Config 3 is the int8 forward reported as ``int8_fwd``; config 4 is
+    inputs and randn tangents; config 3 causal, int8 fwd+bwd.  (Config 3 is the int8 forward reported
+    as ``int8_fwd``; config 4 is
     the multi-GPU run of this script; config 1 is the CPU path, ``cpu_baseline``.)"""
     from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp32
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -192,6 +193,21 @@ def other_configs(n):
     out["cfg2_bf16_fwd_bwd"] = {"shape": [B, H, S, D], "ms": t, "TFLOPs": flop / (t * 1e-3) / 1e12,
                                 "frac_of_bf16_peak": flop / (t * 1e-3) / PEAK_BF16,
                                 "fwd_ms": tf, "fwd_TFLOPs": 4 * B * H * S * S * D / (tf * 1e-3) / 1e12}
+    del q, k, v, dO
+    # config 3 causal (SURVEY §8f N2 extension): int8 fwd+bwd, credited 7·BH·S²·D (half the scores)
+    B, H, S, D = 4, 32, 4096, 128
+    q, k, v = (torch.randn((B, H, S, D), device=dev, generator=g).half() for _ in range(3))
+    dO = (torch.randn((B, H, S, D), device=dev, generator=g) * 1e-3).half()
+
+    def int8_causal_step():
+        O, lse, qi, kiT, vi, sq, sk, sv, km, qb_, kb_ = _int8_forward(q, k, v, smooth=True, images=True,
+                                                                      causal=True)
+        _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb_, kb_, causal=True)
+    t = event_time(int8_causal_step, n)
+    flop = 7.0 * B * H * S * S * D
+    out["cfg3_int8_causal_fwd_bwd"] = {"shape": [B, H, S, D], "ms": t,
+                                       "TOPs": flop / (t * 1e-3) / 1e12,
+                                       "frac_of_int8_peak": flop / (t * 1e-3) / PEAK_I8}
     del q, k, v, dO
     B, H, S, D = 2, 16, 2048, 128
     x = [torch.randn((B, H, S, D), device=dev, generator=g).bfloat16() for _ in range(6)]
