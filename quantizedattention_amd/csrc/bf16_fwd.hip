@@ -33,9 +33,13 @@
 
 namespace qattn {
 
+#ifndef QA_BF_FWD_WAVES
+#define QA_BF_FWD_WAVES 4   // waves (32 queries each) per workgroup
+#endif
+
 template <int D>
 struct Bf16FwdCfg {
-  static constexpr int WAVES = 4;
+  static constexpr int WAVES = QA_BF_FWD_WAVES;
   static constexpr int QROWS = 32 * WAVES;
   static constexpr int KT = 32;                 // keys per ring slot
   static constexpr int NSLOT = 4;
@@ -102,7 +106,7 @@ QA_DEVICE unsigned rne2(float a, float b, float& ra, float& rb) {
 QA_DEVICE float rne1(float a) { return __uint_as_float(pk_bf16(a, a) & 0xffff0000u); }
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void bf16_fwd_kernel(
+__global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
     const _Float16* __restrict__ q, const _Float16* __restrict__ k, const __bf16* __restrict__ v,
     float* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks) {
   using C = Bf16FwdCfg<D>;
