@@ -113,13 +113,27 @@ def ptr(t: torch.Tensor | None):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+class _Stream(ctypes.c_void_p):
+    """A hipStream_t argument that remembers its device (the device guard of ``call``)."""
+    device_index = None
+
+
 def stream_of(t: torch.Tensor):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    st = _Stream(torch.cuda.current_stream(t.device).cuda_stream)
+    st.device_index = t.device.index
+    return st
 
 
 def call(name: str, *args) -> None:
+    """Call a C-ABI entry; launches go to the device of its stream argument (the HIPGuard of SURVEY
+    §8b: ``hipFuncSetAttribute`` and the launch act on the current device)."""
     fn = getattr(load(), name)
-    rc = fn(*args)
+    dev = next((a.device_index for a in args if isinstance(a, _Stream)), None)
+    if dev is not None and dev != torch.cuda.current_device():
+        with torch.cuda.device(dev):
+            rc = fn(*args)
+    else:
+        rc = fn(*args)
     if rc == 1:
         raise QAttnError(f"{name}: unsupported shape/argument (status 1)")
     if rc != 0:

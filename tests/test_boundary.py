@@ -148,3 +148,39 @@ def test_bwd_workspace_size():
     assert lib.qattn_bf16_bwd_ws_bytes(4 * 32, 4096, 4096) == 128 * 128 * 128 * 2048
     assert lib.qattn_bf16_bwd_ws_bytes(6, 96, 160) == 6 * 3 * 5 * 2048
     assert lib.qattn_bf16_bwd_ws_bytes(2, 100, 64) == -1
+
+
+def test_call_guards_the_stream_device(monkeypatch):
+    """_lib.call switches to the device of its stream argument for the launch (host-only check with
+    a stand-in entry point and device hooks)."""
+    import contextlib
+
+    import torch
+
+    from quantizedattention_amd import _lib
+    seen = []
+
+    class FakeLib:
+        @staticmethod
+        def qattn_probe(*args):
+            seen.append(("launch", cur[0]))
+            return 0
+    cur = [0]
+
+    @contextlib.contextmanager
+    def fake_device(i):
+        old, cur[0] = cur[0], i
+        seen.append(("enter", i))
+        yield
+        cur[0] = old
+    monkeypatch.setattr(_lib, "load", lambda: FakeLib)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: cur[0])
+    monkeypatch.setattr(torch.cuda, "device", fake_device)
+    st = _lib._Stream(0)
+    st.device_index = 1
+    _lib.call("qattn_probe", st)
+    assert seen == [("enter", 1), ("launch", 1)]
+    seen.clear()
+    st.device_index = 0
+    _lib.call("qattn_probe", st)
+    assert seen == [("launch", 0)]
