@@ -51,6 +51,17 @@ int qattn_int8_quant_img(const void* x, void* idx, void* scale, void* deq, void*
 int qattn_int8_dequant(const void* idx, const void* scale, void* deq, long rows, int head_dim,
                        void* stream);
 
+/* V quantiser for the int8 P.V product (attention_int8.py:241-247, same indices and scales as
+ * qattn_int8_quant) that also writes the V^T operand image of those indices:
+ *   v f16 [rows, D] -> v_i8 i8 [rows, D], sv f16 [rows/32] (bit-exact, as qattn_int8_quant) and
+ *   vt i8 [rows/32][D/32][64][16]: for each 32-row block and 32-wide d block b, lane L = 32h + c holds
+ *   v_i8[row pi(h, j)][32b + c], j = 0..15, pi(h, j) = (j & 3) + 8(j >> 2) + 4h (the A operand of
+ *   v_mfma_i32_32x32x32_i8 in the forward's key order).  rows % 32 == 0. */
+int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt, long rows, int head_dim,
+                        void* stream);
+/* vt of qattn_int8_quant_vt from stored indices v_i8 (a restored int8 key/value cache). */
+int qattn_int8_v_image(const void* v_i8, void* vt, long rows, int head_dim, void* stream);
+
 /* k_mean = f16(mean over the S tokens of each head) — k f16 [bh*seq, D] -> kmean f16 [bh, D]
  * (SageAttention smoothing; replaces the crashing `k.mean(0)` of attention_int8.py:24-25). */
 int qattn_kmean(const void* k, void* kmean, long bh, long seq, int head_dim, void* stream);
@@ -65,13 +76,24 @@ int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, cons
 
 /* Generalised shapes (the reference's int8 path has none of these): bh = batch *
  * query heads with sq_tok query rows each; the key/value tensors have bh / group heads of sk_tok
- * rows (query head h reads key/value head h / group: grouped-query attention); causal != 0 keeps
- * key <= query (top-left aligned positions), masked scores are excluded.  Block scales index the
+ * rows (query head h reads key/value head h / group: grouped-query attention); causal = 1 keeps
+ * key <= query (top-left aligned positions), causal = 2 keeps key <= query + sk_tok - sq_tok
+ * (bottom-right aligned: new queries against a key/value cache, sk_tok >= sq_tok); masked scores
+ * are excluded.  Block scales index the
  * query rows and the key/value rows separately.  sq_tok % 32 == sk_tok % 32 == 0, bh % group == 0.
  * qattn_int8_attn_fwd is this with sq_tok = sk_tok = seq, group = 1, causal = 0. */
 int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
                            const void* vdq, void* out, void* lse, long bh, long sq_tok, long sk_tok,
                            int group, int causal, int head_dim, float qks, void* stream);
+
+/* qattn_int8_attn_fwd_ex with the P.V contraction on the int8 MFMA, as the reference's
+ * hl.dot(P_int8, v_int8) (attention_int8.py:249): vt = the V^T image of qattn_int8_quant_vt, sv its
+ * block scales; each 32-key tile's exact int32 product is dequantised by sp * sv (int8:249-250).
+ * Same outputs and conventions as qattn_int8_attn_fwd_ex. */
+int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
+                                const void* vt, const void* sv, void* out, void* lse, long bh,
+                                long sq_tok, long sk_tok, int group, int causal, int head_dim,
+                                float qks, void* stream);
 
 /* Backward prologue, one pass (attention_int8.py:372-374, 398): dO f16 -> dO_i8 [rows, D] + sdO f16
  * [rows/32] (same quantiser), dO_bf = bf16(dO_i8) [rows, D] (optional, NULL to skip), and LD f32x2
@@ -262,31 +284,8 @@ int qattn_mxfp4_attn_fwd(const void* q4, const void* qscale, const void* k4, con
                          const void* vt, const void* vscale, void* out, void* lse, long bh, long sq,
                          long sk, int group, int head_dim, float qks, void* stream);
 
-/* ---------------------------------------------------------------- diagnostics (not product API) */
-
-/* qattn_int8_attn_fwd with parts of the tile pipeline disabled (ab = 0 full, 1 no softmax,
- * 2 no P.V, 3 no QK^T, 4 no K/V streaming, 5 = 1+4); D = 128 only.  Output is NOT attention for
- * ab != 0: used by tools/ablate.py to attribute kernel time. */
-int qattn_int8_attn_fwd_ablate(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                               const void* vdq, void* out, void* lse, long bh, long seq, float qks,
-                               int ab, void* stream);
-
-/* MFMA / LDS-transpose fragment-layout probes (one wave; tests/test_gpu_layout.py). */
-int qattn_probe_mfma_i8(const void* A, const void* B, void* C, void* stream);
-int qattn_probe_mfma_f16(const void* A, const void* B, void* C, void* stream);
-int qattn_probe_tr16(const void* M, void* out, void* stream);
-int qattn_probe_pk(const void* x, void* e, void* t, void* stream);
-/* int8-forward softmax helpers on 16 lanes: w = f16(trunc(127 e) * sp) via the round-toward-zero
- * packed fma; d = {f16(a*c + n)} via v_fma_mix (cn holds (c, n) per lane). */
-int qattn_probe_fwd_helpers(const void* e, const void* sp, void* w, const void* a, const void* cn,
-                            void* d, void* stream);
-
-/* MX-FP4 probes: one block-scaled 32x32x64 fp4 MFMA (A, B: 64 lanes x 16 B of e2m1
- * nibbles, sa / sb: one e8m0 byte per lane, C: 64 x 16 f32) and the scaled fp4 pack/unpack converts
- * (lane i packs x[8i..8i+7] with scale s[i]). */
-int qattn_probe_mfma_fp4(const void* A, const void* B, const void* sa, const void* sb, void* C,
-                         void* stream);
-int qattn_probe_fp4_cvt(const void* x, const void* s, void* packed, void* back, void* stream);
+/* Fragment-layout probes and other diagnostics live in a separate development library
+ * (libqattn_dev.so, include/qattn_dev.h); this library exports the product API only. */
 
 #ifdef __cplusplus
 }

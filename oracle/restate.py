@@ -187,7 +187,7 @@ def quant_blocks(x, block=32):
     return idx.reshape(*lead, N, D), s
 
 
-def int8_fwd(q, k, v, block=32, causal=False):
+def int8_fwd(q, k, v, block=32, causal=False, causal_offset=0):
     """Per-(batch, head) restatement of helion_atten_int8_hl_dot_fwd (int8:101-262).
 
     q, k, v fp16 [B,H,S,D], S % 32 == 0.  Returns the reference's 10-tuple
@@ -198,7 +198,9 @@ def int8_fwd(q, k, v, block=32, causal=False):
 
     Extensions (no reference counterpart): k, v may have Hkv = H / G heads (query
     head h reads key/value head h // G) and Sk != S tokens; ``causal`` drops key > query (top-left
-    aligned) by excluding those scores (P = 0; a tile with no kept key has sp = 0).
+    aligned) by excluding those scores (P = 0; a tile with no kept key has sp = 0);
+    ``causal_offset`` shifts the diagonal (query i keeps keys <= i + causal_offset: Sk - Sq aligns the
+    last query with the last key, the key/value-cache decode of SURVEY §8f N3).
     """
     B, H, S, D = q.shape
     Hkv, Sk = k.shape[1], k.shape[2]
@@ -222,7 +224,7 @@ def int8_fwd(q, k, v, block=32, causal=False):
         Sf = ((acc * sqf) * _f(sk[:, t])[:, None, None]) * qks  # int8:200
         S16 = _h(Sf)  # int8:203
         if causal:
-            keep = torch.arange(k0, k1)[None, :] <= torch.arange(S)[:, None]
+            keep = torch.arange(k0, k1)[None, :] <= torch.arange(S)[:, None] + causal_offset
             S16 = torch.where(keep[None], S16, torch.full_like(S16, float("-inf")))
         rm = S16.amax(-1, keepdim=True)  # int8:205
         nm = torch.maximum(m, rm)  # int8:206-209

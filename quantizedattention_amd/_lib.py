@@ -25,9 +25,13 @@ SIGNATURES = {
     "qattn_int8_quant": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_int, _c_int, _vp],
     "qattn_int8_quant_img": [_vp] * 6 + [_c_long, _c_int, _c_int, _vp],
     "qattn_int8_dequant": [_vp, _vp, _vp, _c_long, _c_int, _vp],
+    "qattn_int8_quant_vt": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
+    "qattn_int8_v_image": [_vp, _vp, _c_long, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_int8_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
+    "qattn_int8_attn_fwd_i8pv_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
+                                                 _vp],
     "qattn_int8_attn_bwd_ex": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                              _c_float, _vp],
     "qattn_int8_attn_bwd_ws": [_vp] * 16 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
@@ -63,7 +67,10 @@ SIGNATURES = {
     "qattn_mxfp4_quant_rows": [_vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_mxfp4_quant_vt": [_vp, _vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_mxfp4_attn_fwd": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
-    "qattn_int8_attn_fwd_ablate": [_vp] * 7 + [_c_long, _c_long, _c_float, _c_int, _vp],
+}
+
+# libqattn_dev.so (include/qattn_dev.h): fragment-layout probes for tests/test_gpu_layout.py
+DEV_SIGNATURES = {
     "qattn_probe_mfma_i8": [_vp, _vp, _vp, _vp],
     "qattn_probe_mfma_f16": [_vp, _vp, _vp, _vp],
     "qattn_probe_tr16": [_vp, _vp, _vp],
@@ -77,6 +84,7 @@ SIGNATURES = {
 RESTYPES = {"qattn_int8_bwd_ws_bytes": ctypes.c_long, "qattn_bf16_bwd_ws_bytes": ctypes.c_long}
 
 _lib = None
+_dev = None
 
 
 class QAttnError(RuntimeError):
@@ -104,6 +112,23 @@ def load(path: os.PathLike | None = None) -> ctypes.CDLL:
     return lib
 
 
+def load_dev() -> ctypes.CDLL:
+    """The development library of layout probes (built beside libqattn.so); tests only."""
+    global _dev
+    if _dev is None:
+        load()
+        p = _PKG / "libqattn_dev.so"
+        if not p.exists():
+            raise QAttnError(f"{p} not found: build it with `python -m quantizedattention_amd.build`")
+        lib = ctypes.CDLL(str(p))
+        for name, argtypes in DEV_SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _dev = lib
+    return _dev
+
+
 def exported_symbols() -> list[str]:
     lib = load()
     return [n for n in SIGNATURES if hasattr(lib, n)]
@@ -127,7 +152,7 @@ def stream_of(t: torch.Tensor):
 def call(name: str, *args) -> None:
     """Call a C-ABI entry; launches go to the device of its stream argument (the HIPGuard of SURVEY
     §8b: ``hipFuncSetAttribute`` and the launch act on the current device)."""
-    fn = getattr(load(), name)
+    fn = getattr(load_dev() if name in DEV_SIGNATURES else load(), name)
     dev = next((a.device_index for a in args if isinstance(a, _Stream)), None)
     if dev is not None and dev != torch.cuda.current_device():
         with torch.cuda.device(dev):

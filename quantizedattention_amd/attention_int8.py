@@ -58,13 +58,25 @@ def _check_shapes(q, k, v):
         raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
 
 
-def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = False):
+# P.V contraction of the forward (csrc/int8_attn_fwd.hip):
+#   "i8" (default): v_mfma_i32_32x32x32_i8 on P_i8 x v_i8, as the reference's hl.dot (int8:249), with
+#         one fused dequantisation per 32-key tile; measured the faster mode;
+#   "f16": v_mfma_f32_32x32x16_f16 on f16(P_i8 * sp) x f16(v_i8 * sv), the tile scale in the operands.
+# Same P_i8, scales and tolerance either way; QATTN_INT8_PV selects the default.
+PV_MODE = os.environ.get("QATTN_INT8_PV", "i8")
+
+
+def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = False,
+                  pv: str | None = None):
     """Quantise q, k, v and run the int8 attention forward.
 
     Returns (O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean, q_bf, k_bf); q_bf / k_bf are the exact
     bf16 images of q_i8 / k_i8 the backward reads (written by the same quantiser pass when
-    ``images``, else None).
+    ``images``, else None).  ``pv``: the P.V mode ("f16" / "i8", default PV_MODE).
     """
+    pv = PV_MODE if pv is None else pv
+    if pv not in ("f16", "i8"):
+        raise _lib.QAttnError(f"qattn int8: unknown P.V mode {pv!r} (f16 or i8)")
     _check_shapes(q, k, v)
     _lib.require_gpu(q, k, v)
     q = q.to(torch.float16).contiguous()
@@ -82,7 +94,8 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     sq = torch.empty((N // BQ,), dtype=torch.float16, device=dev)
     sk = torch.empty((Nkv // BKV,), dtype=torch.float16, device=dev)
     sv = torch.empty((Nkv // BKV,), dtype=torch.float16, device=dev)
-    vdq = torch.empty((Nkv, D), dtype=torch.float16, device=dev)  # workspace fp16(v_i8 * sv)
+    # P.V operand image of v: f16(v_i8 * sv) ("f16") or the int8 V^T operand image ("i8")
+    vop = torch.empty((Nkv, D), dtype=torch.float16 if pv == "f16" else torch.int8, device=dev)
     O = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
     lse = torch.empty((N,), dtype=torch.float16, device=dev)
     q_bf = k_bf = None
@@ -97,11 +110,19 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
               None, N, S, D, st)
     _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
               _lib.ptr(k_mean), Nkv, Sk, D, st)
-    _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vdq), None,
-              Nkv, Sk, D, st)
-    _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
-              _lib.ptr(vdq), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, int(bool(causal)), D,
-              float(torch.tensor(_qk_scale(D), dtype=torch.float32)), st)
+    qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
+    if pv == "f16":
+        _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), None,
+                  Nkv, Sk, D, st)
+        _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
+                  _lib.ptr(vop), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, int(bool(causal)),
+                  D, qks, st)
+    else:
+        _lib.call("qattn_int8_quant_vt", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), Nkv,
+                  D, st)
+        _lib.call("qattn_int8_attn_fwd_i8pv_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8),
+                  _lib.ptr(sk), _lib.ptr(vop), _lib.ptr(sv), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk,
+                  H // Hkv, int(bool(causal)), D, qks, st)
     # k_i8T is returned as the [D, N] view of the row-major [N, D] tensor (same values/shape as
     # int8:165, zero-copy).
     return O, lse, q_i8, k_i8.t(), v_i8, sq, sk, sv, k_mean, q_bf, k_bf
@@ -158,8 +179,13 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
               _lib.ptr(q_bf), _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv))
     shape = (B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms, st)
     ws_bytes = _lib.load().qattn_int8_bwd_ws_bytes(B * H, S, Sk)
+    # the records of one key/value head (its H / Hkv query heads) are addressed with 32-bit offsets
+    region_ok = (H // Hkv) * (S // 32) * (Sk // 32) * 1024 < (1 << 31)
     if use_ws is None:
-        use_ws = 0 <= ws_bytes <= WS_MAX_BYTES
+        use_ws = 0 <= ws_bytes <= WS_MAX_BYTES and region_ok
+    elif use_ws and not (region_ok and ws_bytes >= 0):
+        raise _lib.QAttnError("qattn int8 backward: dS workspace region exceeds 2 GiB per key/value "
+                              "head; use the recomputing backward (use_ws=False)")
     ws = None
     if use_ws and ws_bytes > 0:
         try:

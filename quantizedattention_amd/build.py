@@ -16,6 +16,7 @@ CSRC = PKG / "csrc"
 INCLUDE = PKG.parent / "include"
 BUILD = PKG / "_build"
 LIB = PKG / "libqattn.so"
+DEV_LIB = PKG / "libqattn_dev.so"   # fragment-layout probes (csrc/dev): tests only, not product API
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = [
@@ -44,14 +45,19 @@ def _compile(src: Path, obj: Path) -> str:
 
 
 def build(verbose: bool = True, jobs: int = 8) -> Path:
+    _build_lib(sorted(CSRC.glob("*.hip")), LIB, "", verbose, jobs)
+    _build_lib(sorted((CSRC / "dev").glob("*.hip")), DEV_LIB, "dev_", verbose, jobs)
+    return LIB
+
+
+def _build_lib(srcs, lib, prefix: str, verbose: bool, jobs: int) -> None:
     BUILD.mkdir(exist_ok=True)
     headers = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
     hdr_mtime = max((h.stat().st_mtime for h in headers), default=0.0)
-    srcs = sorted(CSRC.glob("*.hip"))
     todo = []
     objs = []
     for s in srcs:
-        o = BUILD / (s.stem + ".o")
+        o = BUILD / (prefix + s.stem + ".o")
         objs.append(o)
         if not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr_mtime):
             todo.append((s, o))
@@ -60,16 +66,15 @@ def build(verbose: bool = True, jobs: int = 8) -> Path:
             for name in ex.map(lambda so: _compile(*so), todo):
                 if verbose:
                     print(f"[qattn build] compiled {name}", file=sys.stderr)
-    if todo or not LIB.exists() or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
-        tmp = LIB.with_suffix(".so.tmp")
+    if todo or not lib.exists() or lib.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        tmp = lib.with_suffix(".so.tmp")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
-        os.replace(tmp, LIB)
+        os.replace(tmp, lib)
         if verbose:
-            print(f"[qattn build] linked {LIB}", file=sys.stderr)
-    return LIB
+            print(f"[qattn build] linked {lib}", file=sys.stderr)
 
 
 if __name__ == "__main__":

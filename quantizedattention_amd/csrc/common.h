@@ -164,6 +164,115 @@ QA_DEVICE _Float16 mul_mix(float a, float c) {
   asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=v"(r) : "v"(a), "v"(c));
   return __builtin_bit_cast(v2h, r)[0];
 }
+// f16(a*c + n), one rounding
+QA_DEVICE _Float16 fma_mix1(float a, float c, float n) {
+  unsigned r;
+  asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[0,0,0]" : "=v"(r) : "v"(a), "v"(c), "v"(n));
+  return __builtin_bit_cast(v2h, r)[0];
+}
+
+// ---------------------------------------------------------------- biased int32 accumulators
+// An int8 MFMA started from C = KMAG_BITS instead of 0 adds the exact integer dot X to the bit
+// pattern of the fp32 value 1.5 * 2^23, whose spacing is 1: read as fp32 the accumulator is exactly
+// KMAG + X for |X| < 2^22 (a 32x32x32 i8 dot is at most 32 * 128 * 128 * (D/32) < 2^22 for D <= 128).
+// The int -> float conversion disappears: f(acc) * c - KMAG * c is X * c in one fused operation, and
+// KMAG * c is exact when c has at most 23 significant bits (kmag_scale clears the last one).  The
+// biased values still order like X as signed int32 (a row max can run on the raw accumulator).
+constexpr int KMAG_BITS = 0x4B400000;
+constexpr float KMAG = 12582912.0f;   // 1.5 * 2^23
+QA_DEVICE float kmag_scale(float c) { return __uint_as_float(__float_as_uint(c) & ~1u); }
+
+// d[j] = {f16(a[2j]*c + n), f16(a[2j+1]*c + n)} for the 16 values of a biased accumulator (the same
+// v_fma_mix rounding as fma_mix8).  `dep` must be a value the compiler computed FROM those
+// accumulator registers (e.g. their row max): hipcc inserts the MFMA-result -> VALU wait states only
+// for its own instructions, so this asm has to be ordered after one of them; the operand makes it so.
+QA_DEVICE void fma_mix16_after(const v16i& acc, float c, float n, int dep, v2h* d) {
+  float a[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = __int_as_float(acc[i]);
+  unsigned r[8];
+  asm("v_fma_mixlo_f16 %0, %8, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, %10, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %2, %12, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %3, %14, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %4, %16, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %5, %18, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %6, %20, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %7, %22, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %9, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, %11, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %2, %13, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %3, %15, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %4, %17, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %5, %19, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %6, %21, %24, %25 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %7, %23, %24, %25 op_sel_hi:[0,0,0]"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
+        "=&v"(r[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
+        "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]),
+        "v"(a[15]), "v"(c), "v"(n), "v"(dep));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = __builtin_bit_cast(v2h, r[j]);
+}
+// f32(x.lo) + f32(x.hi) of a packed f16 pair in one v_fma_mix_f32
+QA_DEVICE float pk_hsum(v2h x) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, 1.0, %1 op_sel:[0,0,1] op_sel_hi:[1,0,1]"
+      : "=v"(r) : "v"(__builtin_bit_cast(unsigned, x)));
+  return r;
+}
+// y = RTZ_f16(w * e + 1024) = 1024 + trunc(w * e) for 0 <= w * e < 1024 (the f16 spacing is 1 in
+// [1024, 2048)): byte 0 / byte 2 of y are the int8 indices trunc(w * e) of the two halves.
+// MODE.FP_ROUND[3:2] (f16/f64) = 3 (toward zero) only around the 8 ops.
+QA_DEVICE void p_index8(const v2h* e, v2h w2, unsigned* y) {
+  const v2h k1024 = {(_Float16)1024.0f, (_Float16)1024.0f};
+  asm("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\t"
+      "s_nop 1\n\t"
+      "v_pk_fma_f16 %0, %8, %16, %17\n\t"
+      "v_pk_fma_f16 %1, %9, %16, %17\n\t"
+      "v_pk_fma_f16 %2, %10, %16, %17\n\t"
+      "v_pk_fma_f16 %3, %11, %16, %17\n\t"
+      "v_pk_fma_f16 %4, %12, %16, %17\n\t"
+      "v_pk_fma_f16 %5, %13, %16, %17\n\t"
+      "v_pk_fma_f16 %6, %14, %16, %17\n\t"
+      "v_pk_fma_f16 %7, %15, %16, %17\n\t"
+      "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 0\n\t"
+      "s_nop 1"
+      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(y[4]), "=&v"(y[5]), "=&v"(y[6]),
+        "=&v"(y[7])
+      : "v"(e[0]), "v"(e[1]), "v"(e[2]), "v"(e[3]), "v"(e[4]), "v"(e[5]), "v"(e[6]), "v"(e[7]),
+        "v"(w2), "v"(k1024));
+}
+// Pack the int8 indices of p_index8 into the i8 MFMA operand: byte j = index j (j = 0..15), i.e.
+// byte 0 of y[j/2] half j%2.
+QA_DEVICE v4i pack_p_index(const unsigned* y) {
+  v4i r;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) r[w] = (int)__builtin_amdgcn_perm(y[2 * w + 1], y[2 * w], 0x06040200u);
+  return r;
+}
+// The low bytes of the 16 int32 values of an accumulator, packed in register order (byte j of the
+// result = low byte of t[j]): the i8 operand of a following MFMA.
+QA_DEVICE v4i pack_acc_bytes(const v16i& t) {
+  v4i r;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const unsigned lo = __builtin_amdgcn_perm((unsigned)t[4 * w + 1], (unsigned)t[4 * w], 0x0c0c0400u);
+    const unsigned hi = __builtin_amdgcn_perm((unsigned)t[4 * w + 3], (unsigned)t[4 * w + 2], 0x0c0c0400u);
+    r[w] = (int)__builtin_amdgcn_perm(hi, lo, 0x05040100u);
+  }
+  return r;
+}
+// B operand of the 32x32 identity for v_mfma_i32_32x32x32_i8: lane l holds B[k = 16h + j][l & 31],
+// byte j = (16h + j == l & 31).  X . I with X as the A operand (lane = row, 16 consecutive k bytes)
+// returns X in the accumulator layout (lane = column, rows in registers): a register transpose.
+QA_DEVICE v4i identity_b_i8(int lane) {
+  const int j = (lane & 31) - 16 * (lane >> 5);
+  v4i r = {0, 0, 0, 0};
+  if (j >= 0 && j < 16) r[j >> 2] = 1 << (8 * (j & 3));
+  return r;
+}
 // y = RTZ_f16(127 e + 1024) = P_i8 + 1024 (exact integer), then w = RNE_f16(y*sp - 1024*sp) =
 // f16(P_i8 * sp).  MODE.FP_ROUND[3:2] (f16/f64) = 3 (toward zero) only around the first 8 ops.
 QA_DEVICE void p_operand8(const v2h* e, v2h sp2, v2h nsp2, v2h* w) {
@@ -245,7 +354,7 @@ QA_DEVICE void ring_wait_barrier() {
 // + soffset (wave-uniform tile offset, SGPR); LDS destination = M0 + 16*lane (4*lane for dword).
 // Per piece only the M0 write and the load issue: no 64-bit per-lane address arithmetic.  M0 is
 // written without save/restore: the kernels that use these helpers contain no other M0 use
-// (tests/test_isa.py checks the disassembly), and the M0 -> LDS-DMA hazard takes one s_nop.
+// (tests/test_isa.py checks the disassembly of every kernel that uses them), and the M0 -> LDS-DMA hazard takes one s_nop.
 QA_DEVICE v4u make_rsrc(const void* base, unsigned bytes) {
   const unsigned long a = (unsigned long)base;
   v4u r;
@@ -327,8 +436,10 @@ struct RowTile {
   static constexpr int PITCH = DC * (int)sizeof(T) + 16;
   static constexpr int BYTES = 32 * PITCH;
 };
-template <int D, typename T, int NPASS = 1>
-QA_DEVICE void store_rows(const v16f* acc, float sc, char* lds, T* dst_row0, int lane) {
+// Element value written: acc * sc, or fma(acc, sc, add) when AFFINE.
+template <int D, typename T, int NPASS = 1, bool AFFINE = false>
+QA_DEVICE void store_rows(const v16f* acc, float sc, char* lds, T* dst_row0, int lane,
+                          float add = 0.f) {
   using RT = RowTile<D, T, NPASS>;
   constexpr int NBP = D / 32 / NPASS;                        // 32-wide d blocks per pass
   const int h = lane >> 5, c32 = lane & 31;
@@ -343,12 +454,14 @@ QA_DEVICE void store_rows(const v16f* acc, float sc, char* lds, T* dst_row0, int
         if constexpr (sizeof(T) == 2) {
           v4h w;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * sc);
+          for (int j = 0; j < 4; ++j)
+            w[j] = (_Float16)(AFFINE ? fmaf(acc[b][4 * g + j], sc, add) : acc[b][4 * g + j] * sc);
           *reinterpret_cast<v4h*>(p) = w;
         } else {
           v4f w;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) w[j] = acc[b][4 * g + j] * sc;
+          for (int j = 0; j < 4; ++j)
+            w[j] = AFFINE ? fmaf(acc[b][4 * g + j], sc, add) : acc[b][4 * g + j] * sc;
           *reinterpret_cast<v4f*>(p) = w;
         }
       }

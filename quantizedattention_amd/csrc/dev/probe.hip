@@ -1,7 +1,8 @@
 // Fragment-layout probes: one-wave GEMM tiles that load operands with the lane maps assumed in
 // common.h and store C with the assumed C/D map.  tests/test_gpu_layout.py checks them against a
 // CPU matmul on asymmetric integer data (cdna_hip_programming.md §3: "A=I-check with ASYMMETRIC B").
-#include "common.h"
+#include "../common.h"
+#include "qattn_dev.h"
 
 namespace qattn {
 

@@ -3,34 +3,46 @@
 //
 // Work decomposition
 //   * one workgroup = 4 waves = 128 query rows of one (b,h); wave w owns rows 32w..32w+31 = one
-//     32-token q-quant block (one sq scale per wave).  3 workgroups per CU (<= 168 VGPRs).
-//   * keys stream in 32-key tiles (= one Bkv block) through a 4-slot LDS ring filled by LDS-DMA
-//     (global_load_lds_dwordx4: no staging registers; the bank swizzle is applied to the per-lane
-//     source address, the LDS image is written lane-linearly).  One barrier per tile; the DMA of
-//     tile t+3 is issued right after the barrier of tile t (two tiles of latency cover).
-//   * every sk scale of the head sits in LDS (loaded once); workgroups of one head share an XCD.
+//     32-token q-quant block (one sq scale per wave).  PV_I8: 2 workgroups per CU (<= 256 VGPRs);
+//     PV_F16: 3 (<= 168 VGPRs).
+//   * keys stream in 32-key tiles (= one Bkv block) through a 4-slot LDS ring filled by buffer
+//     LDS-DMA (no staging registers; the bank swizzle is applied to the per-lane source offset, the
+//     LDS image is written lane-linearly).  One barrier per tile; the DMA of tile t+3 is issued
+//     right after the barrier of tile t.
+//   * per-tile scales of the head sit in LDS (loaded once); workgroups of one head share an XCD.
 //
 // Per 32-key tile and wave (swapped orientation: keys in registers, query on the lane pair l, l^32),
 // software-pipelined by one tile so that each wave has MFMA work beside its softmax VALU:
-//     QK(t+1)   S^T = K_i8 . Q_i8^T            D/32 x v_mfma_i32_32x32x32_i8
-//     SM2(t)    e = exp2(d), l, P operand        (VALU, beside the QK(t+1) MFMAs)
-//     PV(t)     O^T += Vdq^T . P^T               2*D/32 x v_mfma_f32_32x32x16_f16
-//     SM1(t+1)  d = S - rowmax, deferred max     (VALU, beside the PV(t) MFMAs)
-// Reference rounding points (int8:197-257), with S never materialised:
-//     S  = f16(acc * c)          (one v_fma_mix per element: exact product, one f16 rounding)
-//     rm = f16(max_k(acc) * c)   (c = sq*sk*qks > 0: the row max commutes with the monotone scaling)
-//     d  = f16(S - rm)           (S is rounded to f16 first, as the reference does: rounding
-//                                 acc*c - rm once instead changes trunc(127 e) for many scores)
-//     e  = exp2(d);  P_i8 = trunc(127 e);  operand = f16(P_i8 * sp),  sp = exp2(rm - m)/127
-//     P_i8 + 1024 = (127 e + 1024) rounded toward zero (f16 spacing 1 in [1024, 2048)); the operand
-//     is then one fma  f16((P_i8 + 1024)*sp - 1024*sp)  -> 2 packed ops per element pair.
+//     QK(t+1)   S^T = K_i8 . Q_i8^T                   D/32 x v_mfma_i32_32x32x32_i8
+//     SM2(t)    e = exp2(d), l, P operand             (VALU, beside the QK(t+1) MFMAs)
+//     PV(t)     O^T += V^T . P^T                      (PV modes below)
+//     SM1(t+1)  d = S - rowmax, deferred running max  (VALU, beside the PV(t) MFMAs)
+// Reference rounding points (int8:197-257):
+//     S  = f16(acc * c),  c = sq*sk*qks          one v_fma_mix per score on the biased accumulator
+//                                                (common.h KMAG: no int -> float conversion)
+//     rm = f16(max_k(acc) * c)                   (c > 0: the row max commutes with the scaling)
+//     d  = f16(S - rm)                           (S rounded to f16 first, as the reference does)
+//     e  = exp2(d);  P_i8 = trunc(127 e);  sp = exp2(rm - m)/127  (int8:211-237)
 //     l += exp2(rm - m) * sum e (fp32);  O *= exp2(m_old - m) when the running max moves.
-// Vdq = fp16(v_i8 * sv) is written by the quantiser, so the fp32 accumulation of
-// sum_t sp*sv*(P_i8 . v_i8) (int8:249-250) runs inside the MFMA, exact up to the fp16 rounding of
-// the two dequantised operands.
 // Deferred max (cdna_hip_programming.md T13): the running max m moves only when some row's tile max
 // exceeds it by more than THR = 8 (log2 units); P_i8 depends only on S - rowmax(tile), O and l share
-// the (possibly stale) reference, so O / l is unchanged up to rounding and operands stay <= 2^8.
+// the (possibly stale) reference, so O / l is unchanged up to rounding.
+//
+// P.V modes (int8:249-250, O += (P_i8 . v_i8) * sp * sv per 32-key tile):
+//   PV_F16            one v_mfma_f32_32x32x16_f16 chain on f16(P_i8 * sp) x f16(v_i8 * sv) (the
+//                     quantiser's vdq image): the tile scale rides in the operands, the fp32
+//                     accumulator needs no per-tile work.  P_i8 and the scales are the reference's;
+//                     the extra rounding is that of the two f16 products.
+//   PV_I8 (default)   the literal reference contraction: v_mfma_i32_32x32x32_i8 on P_i8 x v_i8 (V^T
+//                     operand image vt from qattn_int8_quant_vt), exact int32 per tile, then one
+//                     fused dequantisation per accumulator element and tile, O += acc * sp*sv
+//                     (biased accumulator: 1 VALU per element instead of 2).
+//   Both keep the reference's per-32-key P quantisation; coarser P.V blocks (one dequantisation per
+//   2 or 4 tiles) move O by 1.3e-2 .. 6e-2 from the reference (tools/pv_quant_study.py: the
+//   truncation bias grows with the block), past the 1e-2 bar.  PV_I8 spends 32 packed fp32 FMAs per
+//   wave-tile on the dequantisation but streams half the V bytes (int8 image, 4 KiB per tile through
+//   DMA and LDS instead of 8) and issues 8 MFMAs instead of 12: measured 15-18 % faster than PV_F16
+//   at config 3.
 #include <climits>
 #include <type_traits>
 
@@ -38,63 +50,84 @@
 
 namespace qattn {
 
-#ifndef QA_FWD_OCC
-#define QA_FWD_OCC 3
+enum PvMode { PV_F16 = 0, PV_I8 = 1 };
+
+// A/B knobs (tools/ab_build.sh, tools/ab_time.py; measured on MI355X):
+//   QA_FWD_WAVES    waves (32 query rows each) per workgroup.  8 halve the L2 -> LDS bytes per
+//                   query but measured 2-3 % slower than 4.
+//   QA_FWD_OCC_F16  workgroups per CU of the PV_F16 kernel (3: <= 168 VGPRs, 2: <= 256).
+//   QA_FWD_QK_BIAS  -1 (default): the biased S accumulator (one v_fma_mix per score) in PV_I8 (which
+//                   keeps the 16-register seed for its P.V anyway), the int32 -> fp32 conversion in
+//                   PV_F16 (whose 168-VGPR budget the seed would overflow into scratch); 0 / 1 force it.
+#ifndef QA_FWD_WAVES
+#define QA_FWD_WAVES 4
 #endif
-#ifndef QA_FWD_UNROLL
-#define QA_FWD_UNROLL 0
+#ifndef QA_FWD_OCC_F16
+#define QA_FWD_OCC_F16 3
+#endif
+#ifndef QA_FWD_QK_BIAS
+#define QA_FWD_QK_BIAS -1
 #endif
 
-template <int D>
+template <int D, int PV>
 struct Int8FwdCfg {
-  static constexpr int WAVES = 4;
+  static constexpr int WAVES = QA_FWD_WAVES;
   static constexpr int QROWS = 32 * WAVES;      // query rows per workgroup
   static constexpr int KT = 32;                 // keys per tile / ring slot
   static constexpr int NSLOT = 4;               // ring slots
   static constexpr int K_BYTES = KT * D;        // int8 K tile
-  static constexpr int V_BYTES = KT * D * 2;    // fp16 Vdq tile
+  static constexpr int V_BYTES = PV == PV_F16 ? KT * D * 2 : KT * D;   // f16 vdq / i8 V^T image
   static constexpr int SLOT = K_BYTES + V_BYTES;
   static constexpr int NKS = D / 32;            // i8 k-steps for QK^T
   static constexpr int NDB = D / 32;            // 32-wide d blocks of O^T
   static constexpr int K_CH = D / 16;           // 16-B chunks per K row
-  static constexpr int V_CH = D * 2 / 16;       // 16-B chunks per V row
+  static constexpr int V_CH = D * 2 / 16;       // 16-B chunks per vdq row
   static constexpr int K_SW_SHIFT = (D == 128) ? 1 : 2;
   static constexpr int V_SW_SHIFT = (D == 128) ? 2 : 1;
   static constexpr int K_INST = K_BYTES / 1024; // 1-KiB LDS-DMA wave instructions per tile
   static constexpr int V_INST = V_BYTES / 1024;
   static constexpr int INST = K_INST + V_INST;
   static constexpr int IPW = (INST + WAVES - 1) / WAVES;   // per wave, padded (counted vmcnt)
+  // waves per SIMD the register budget must allow (__launch_bounds__ second argument): two (<= 256
+  // VGPRs), three for the PV_F16 kernel at QA_FWD_OCC_F16 = 3 with 4-wave workgroups
+  static constexpr int WPS = (PV == PV_F16 && WAVES == 4) ? QA_FWD_OCC_F16 : 2;
+  static constexpr bool QK_BIAS = QA_FWD_QK_BIAS < 0 ? PV == PV_I8 : QA_FWD_QK_BIAS != 0;
+  // the ring, reused as the output staging area of the epilogue
+  static constexpr int STAGE = WAVES * RowTile<D, _Float16>::BYTES;
+  static constexpr int RING = NSLOT * SLOT > STAGE ? NSLOT * SLOT : STAGE;
   static constexpr float THR = 8.0f;
 };
 
 template <int D>
 QA_DEVICE int k_sw(int row) {
-  using C = Int8FwdCfg<D>;
-  return (row >> C::K_SW_SHIFT) & (C::K_CH - 1);
+  constexpr int K_CH = D / 16;
+  return (row >> ((D == 128) ? 1 : 2)) & (K_CH - 1);
 }
 template <int D>
 QA_DEVICE int v_sw(int row) {
-  using C = Int8FwdCfg<D>;
-  return (row & 3) << C::V_SW_SHIFT;
+  return (row & 3) << ((D == 128) ? 2 : 1);
 }
 
-// LDS-DMA plan of one 32-key tile (K rows then V rows), IPW instructions per wave.  Waves whose
-// padded slots run past INST re-issue their first instruction (same bytes to the same place:
+// LDS-DMA plan of one 32-key tile (K rows, then the V operand), IPW instructions per wave.  Waves
+// whose padded slots run past INST re-issue their first instruction (same bytes to the same place:
 // benign), so every wave has exactly IPW DMAs in flight per tile and vmcnt(IPW) means "all but the
 // last tile".  Per instruction: a lane-constant source byte offset (swizzle applied), a wave-uniform
-// LDS offset inside the slot and whether it reads V; the tile's base pointers are scalar.
-template <int D>
+// LDS offset inside the slot and the tile stride; the tile's base pointers are scalar.
+//   K: row-major int8 rows, 16-B chunks XOR-swizzled by row.
+//   V, PV_F16: row-major f16 vdq rows, swizzled for the transposed ds_read_b64_tr_b16 reads.
+//   V, PV_I8: the vt operand image, already in MFMA-operand order: a plain 1-KiB copy per piece.
+template <int D, int PV>
 struct DmaPlan {
-  using C = Int8FwdCfg<D>;
+  using C = Int8FwdCfg<D, PV>;
   unsigned voff[C::IPW];
   unsigned lds_off[C::IPW];
   unsigned stride[C::IPW];
   v4u rsrc[C::IPW];
-  QA_DEVICE void init(int wave, int lane, int S, const int8_t* kbase, const _Float16* vbase) {
+  QA_DEVICE void init(int wave, int lane, int S, const int8_t* kbase, const void* vbase) {
 #pragma unroll
     for (int i = 0; i < C::IPW; ++i) {
       int inst = wave + C::WAVES * i;
-      if (inst >= C::INST) inst = wave;
+      if (inst >= C::INST) inst = wave % C::INST;   // (more waves than pieces: re-issue one)
       if (inst < C::K_INST) {
         constexpr int RPI = 64 / C::K_CH;
         const int row = inst * RPI + lane / C::K_CH, p = lane % C::K_CH;
@@ -102,7 +135,7 @@ struct DmaPlan {
         lds_off[i] = inst * 1024;
         stride[i] = C::K_BYTES;
         rsrc[i] = make_rsrc(kbase, (unsigned)S * D);
-      } else {
+      } else if constexpr (PV == PV_F16) {
         const int vi = inst - C::K_INST;
         constexpr int RPI = 64 / C::V_CH;
         const int row = vi * RPI + lane / C::V_CH, p = lane % C::V_CH;
@@ -110,6 +143,12 @@ struct DmaPlan {
         lds_off[i] = C::K_BYTES + vi * 1024;
         stride[i] = C::V_BYTES;
         rsrc[i] = make_rsrc(vbase, (unsigned)S * 2 * D);
+      } else {
+        const int vi = inst - C::K_INST;
+        voff[i] = vi * 1024 + 16 * lane;
+        lds_off[i] = C::K_BYTES + vi * 1024;
+        stride[i] = C::V_BYTES;
+        rsrc[i] = make_rsrc(vbase, (unsigned)S * D);
       }
     }
   }
@@ -123,36 +162,34 @@ struct DmaPlan {
 // (compiles to v_max3_i32).  Deliberately NOT inline asm: its inputs are MFMA results, and hipcc's
 // hazard recogniser inserts the MFMA-result -> VALU wait states only for instructions it emits itself.
 QA_DEVICE int imax3(int a, int b, int c) { return max(max(a, b), c); }
-#if defined(QA_FWD_STAMP)
-__device__ unsigned long long g_fwd_stamps[32 * 4 * 64 * 8];
-__device__ unsigned long long g_fwd_wginfo[8192 * 4];
-#endif
 
 // Per-wave softmax state between the two halves of a tile.
 struct SmTile {
   v2h d[8];       // f16(S - rm) for the 16 scores of this lane
   float er;       // exp2(rm - m)
-  _Float16 sp;    // f16(er / 127)
+  float cpv;      // PV_F16: sp = f16(er / 127) (as f32); PV_I8: the tile's dequantisation er/127*sv
 };
 
-// AB (diagnostic timing builds only, never dispatched by the API): 1 = no softmax VALU,
-// 2 = no PV MFMA, 3 = no QK^T MFMA, 4 = no K/V streaming (ring slot 0 reused, no barriers),
-// 5 = 4 + no softmax, 6 = 1 + half the V-operand LDS reads, 7 = 1 + half the K-operand LDS reads.
-// Outputs of AB != 0 are meaningless.
 // Shapes: BH = batch * query heads, Sq query and Sk key tokens per head; query head
-// bh reads key/value head bh / G (grouped-query attention, G = Hq / Hkv).  CAUSAL keeps key <= query
-// (top-left aligned indices); masked scores are excluded (P = 0).  The reference has neither (its
-// int8 path is square, ungrouped and non-causal, int8:122-127, 344); these are extensions.
-template <int D, int AB = 0, bool CAUSAL = false>
-__global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
+// bh reads key/value head bh / G (grouped-query attention, G = Hq / Hkv).  CAUSAL keeps key <=
+// query + qoff: qoff = 0 aligns the first query with the first key (top-left), qoff = Sk - Sq the
+// last with the last (bottom-right: new queries against a key/value cache); masked
+// scores are excluded (P = 0).  The reference has neither (its int8 path is square, ungrouped and
+// non-causal, int8:122-127, 344); these are extensions.
+// vop: PV_F16 the vdq image f16 [BHkv*Sk, D]; PV_I8 the vt image (qattn_int8_quant_vt).
+// (the causal PV_F16 kernel's diagonal masking does not fit 168 VGPRs: 2 waves per SIMD)
+template <int D, int PV, bool CAUSAL>
+constexpr int fwd_wps() { return CAUSAL ? 2 : Int8FwdCfg<D, PV>::WPS; }
+template <int D, int PV, bool CAUSAL>
+__global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CAUSAL>())) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
-    const _Float16* __restrict__ sk, const _Float16* __restrict__ vdq, _Float16* __restrict__ out,
-    _Float16* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks) {
-  using C = Int8FwdCfg<D>;
-  constexpr bool STREAM = AB != 4 && AB != 5;
-  constexpr bool SOFTMAX = AB != 1 && AB != 5 && AB != 6 && AB != 7;
+    const _Float16* __restrict__ sk, const void* __restrict__ vop, const _Float16* __restrict__ sv,
+    _Float16* __restrict__ out, _Float16* __restrict__ lse, int BH, int Sq, int Sk, int G, int qoff,
+    float qks) {
+  using C = Int8FwdCfg<D, PV>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  _Float16* sk_lds = reinterpret_cast<_Float16*>(smem + C::NSLOT * C::SLOT);
+  // per-tile scales: ck = sk * qks (f32); PV_I8 also sv / 127 (f32)
+  float* ck_lds = reinterpret_cast<float*>(smem + C::RING);
 
   const int nq = (Sq + C::QROWS - 1) / C::QROWS;
   int bh, qt;
@@ -167,38 +204,48 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
   const long head_row0 = (long)bh * Sq;           // this head's query rows
   const long kv_row0 = (long)(bh / G) * Sk;       // its key/value head's rows
   const int8_t* kbase = k_i8 + kv_row0 * D;
-  const _Float16* vbase = vdq + kv_row0 * D;
+  const void* vbase = PV == PV_F16
+      ? (const void*)(reinterpret_cast<const _Float16*>(vop) + kv_row0 * D)
+      : (const void*)(reinterpret_cast<const int8_t*>(vop) + kv_row0 * D);
   // causal: key tiles past the workgroup's last query are masked for all of its rows
-  const int nt = CAUSAL ? min(Sk / C::KT, (qt * C::QROWS + C::QROWS) / C::KT) : Sk / C::KT;
+  const int nt = CAUSAL ? min(Sk / C::KT, (qt * C::QROWS + C::QROWS + qoff + C::KT - 1) / C::KT)
+                        : Sk / C::KT;
+  float* svq_lds = ck_lds + nt;
 
-  DmaPlan<D> dma;
+  DmaPlan<D, PV> dma;
   dma.init(wave, lane, Sk, kbase, vbase);
   const unsigned smem_lds = lds_addr(smem);
   dma.issue(smem_lds, 0);
-  if (STREAM) {
-    dma.issue(smem_lds + 1 * C::SLOT, min(1, nt - 1));
-    dma.issue(smem_lds + 2 * C::SLOT, min(2, nt - 1));
+  dma.issue(smem_lds + 1 * C::SLOT, min(1, nt - 1));
+  dma.issue(smem_lds + 2 * C::SLOT, min(2, nt - 1));
+  for (int i = tid; i < nt; i += 64 * C::WAVES) {
+    ck_lds[i] = (float)sk[kv_row0 / 32 + i] * qks;
+    if constexpr (PV == PV_I8) svq_lds[i] = (float)sv[kv_row0 / 32 + i] * (1.0f / 127.0f);
   }
-  for (int i = tid; i < nt; i += 64 * C::WAVES) sk_lds[i] = sk[kv_row0 / 32 + i];
 
   // ---- Q fragment (B operand of S^T = K Q^T): lane holds Q[q0+c32][32s + 16h .. +16]
   v4i qf[C::NKS];
-  float sqw = 0.f;
+  float cq = 0.f;
   if (active) {
     const int8_t* qrow = q_i8 + (head_row0 + q0 + c32) * D + 16 * h;
 #pragma unroll
     for (int s = 0; s < C::NKS; ++s) qf[s] = *reinterpret_cast<const v4i*>(qrow + 32 * s);
-    sqw = (float)sq[(head_row0 + q0) / 32];
+    cq = (float)sq[(head_row0 + q0) / 32];
   }
-  const float cq = sqw * qks;
+  // the biased accumulator seed, opaque to the compiler (so it stays in 16 registers instead of
+  // being re-materialised by 16 v_mov per use)
+  v16i kmag;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) kmag[i] = KMAG_BITS;
+  asm volatile("" : "+v"(kmag));
 
-  // lane-constant LDS byte offsets (the swizzles depend only on row bits fixed per lane):
-  //   K A-operand chunk (2s+h) of key row c32;  V^T A-operand, d-block b: key rows 4h + (i16>>2)
-  //   (+16 per k-step, +8 for the 2nd read), columns 32b + 16gg + 4(i16&3)
+  // lane-constant LDS byte offsets: K A-operand chunk (2s+h) of key row c32; PV_F16: V^T A-operand
+  // of d-block b: key rows 4h + (i16>>2) (+16 per k-step, +8 for the 2nd read), columns
+  // 32b + 16gg + 4(i16&3); PV_I8: piece b of the vt image, 16 B per lane
   int koff[C::NKS], voff[C::NDB];
 #pragma unroll
   for (int s = 0; s < C::NKS; ++s) koff[s] = c32 * D + 16 * ((2 * s + h) ^ k_sw<D>(c32));
-  {
+  if constexpr (PV == PV_F16) {
     const int gg = (lane >> 4) & 1, i16 = lane & 15;
     const int key_a = 4 * h + (i16 >> 2);
 #pragma unroll
@@ -206,63 +253,45 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
       voff[b] = C::K_BYTES + key_a * 2 * D + 16 * ((d / 8) ^ v_sw<D>(key_a)) + (d % 8) * 2;
     }
+  } else {
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) voff[b] = C::K_BYTES + b * 1024 + 16 * lane;
   }
 
   v16f o[C::NDB];
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) o[b] = v16f{};
   _Float16 m = (_Float16)(-INFINITY);
-  float l = 0.f;  // per-lane partial (this lane's key half); the reference's l = 1 is wiped by r = 0
+  float l = 0.f;      // per-lane partial (this lane's key half); the reference's l = 1 is wiped by r = 0
+  float obias = 0.f;  // PV_I8: sum of the tile dequantisation factors (the KMAG bias of O is KMAG * obias)
 
-  // ring slot of a tile: a runtime tile index (slot t & 3), or, with QA_FWD_UNROLL, the slot as a
-  // compile-time constant (every LDS offset becomes a lane-constant VGPR plus an immediate)
-  auto slot_idx = [](auto t) -> int {
-    if constexpr (std::is_integral_v<decltype(t)>) return t & 3;
-    else return decltype(t)::value;
-  };
-  auto slot_of = [&](auto t) -> const char* { return smem + (STREAM ? slot_idx(t) : 0) * C::SLOT; };
+  auto slot_of = [&](int t) -> const char* { return smem + (t & (C::NSLOT - 1)) * C::SLOT; };
 
-  // S^T tile t into an int32 accumulator: fragment loads and MFMAs separately, so the K loads of
-  // tile t+1 can be issued ahead of the V-operand loads of tile t
-  auto qk_load = [&](auto t, v4i* kf) {
+  // S^T tile t into a biased int32 accumulator: fragment loads and MFMAs separately, so the K loads
+  // of tile t+1 can be issued ahead of the V-operand loads of tile t
+  auto qk_load = [&](int t, v4i* kf) {
     const char* kl = slot_of(t);
 #pragma unroll
-    for (int s = 0; s < C::NKS; ++s) {
-      if (AB == 7 && s >= C::NKS / 2) kf[s] = kf[s - C::NKS / 2] + 1;   // half the K reads (timing)
-      else kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s]);
-    }
+    for (int s = 0; s < C::NKS; ++s) kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s]);
   };
   auto qk_mma = [&](const v4i* kf) -> v16i {
-    v16i acc;
-    if constexpr (AB == 3) {
+    v16i acc = mfma_i8(kf[0], qf[0], C::QK_BIAS ? kmag : v16i{});
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = kf[i & 3][i >> 2] + qf[i & 3][0];
-    } else {
-      acc = mfma_i8(kf[0], qf[0], v16i{});
-#pragma unroll
-      for (int s = 1; s < C::NKS; ++s) acc = mfma_i8(kf[s], qf[s], acc);
-    }
+    for (int s = 1; s < C::NKS; ++s) acc = mfma_i8(kf[s], qf[s], acc);
     return acc;
   };
-  auto qk = [&](int t) -> v16i {
-    v4i kf[C::NKS];
-    qk_load(t, kf);
-    return qk_mma(kf);
-  };
 
-  // first half of the softmax of a tile (c = sq*sk*qks of the tile):
-  //   (a) row max of the int32 scores and d = f16(S - rm): independent of the running max, so it
-  //       shares a basic block with the PV MFMAs of the previous tile;
-  //   (b) deferred running-max update (rare branch), er = exp2(rm - m), sp = f16(er / 127).
-  auto sm1a = [&](const v16i& acc_in, float c, SmTile& st, int t) -> _Float16 {
+  // first half of the softmax of tile t: row max, d = f16(S - rm), deferred running max, er, and
+  // the tile's P.V scale
+  auto sm1 = [&](const v16i& acc_in, int t, SmTile& st) {
     // causal tiles crossing this wave's diagonal: keys above the row's query drop out of the max
-    // (INT_MIN) and get d = -inf below, so P = 0 and the tile scale sp ignores them
-    const bool diag = CAUSAL && (t * C::KT + C::KT - 1 > q0);
+    // (INT_MIN) and get d = -inf below, so P = 0 and the tile scale ignores them
+    const bool diag = CAUSAL && (t * C::KT + C::KT - 1 > q0 + qoff);
     v16i acc = acc_in;
     if (diag) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (t * C::KT + (r & 3) + 8 * (r >> 2) + 4 * h > q0 + c32) acc[r] = INT_MIN;
+        if (t * C::KT + (r & 3) + 8 * (r >> 2) + 4 * h > q0 + qoff + c32) acc[r] = INT_MIN;
     }
     int mx = imax3(acc[0], acc[1], acc[2]);
     mx = imax3(mx, acc[3], acc[4]);
@@ -276,13 +305,21 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
       auto r = __builtin_amdgcn_permlane32_swap((unsigned)mx, (unsigned)mx, false, false);
       mx = max((int)r[0], (int)r[1]);
     }
-    // S = f16(f32(acc * c)) (int8:200-203: fp32 products, then fp16); v_mul + v_cvt_pk_f16_f32 is
-    // cheaper than v_fma_mix (tools/ubench) and rounds like the reference's fp32 chain
-    const _Float16 rm = (_Float16)((float)mx * c);
+    // S = f16(X * c) (int8:200-203: fp32 products, then fp16)
     v2h s2[8];
+    _Float16 rm;
+    if constexpr (C::QK_BIAS) {   // on the biased accumulator: one v_fma_mix per score
+      const float c = kmag_scale(cq * ck_lds[t]);
+      const float nb = -KMAG * c;
+      rm = fma_mix1(__int_as_float(mx), c, nb);
+      fma_mix16_after(acc, c, nb, mx, s2);
+    } else {
+      const float c = cq * ck_lds[t];
+      rm = (_Float16)((float)mx * c);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      s2[j] = __builtin_bit_cast(v2h, pk_f16((float)acc[2 * j] * c, (float)acc[2 * j + 1] * c));
+      for (int j = 0; j < 8; ++j)
+        s2[j] = __builtin_bit_cast(v2h, pk_f16((float)acc[2 * j] * c, (float)acc[2 * j + 1] * c));
+    }
     const v2h rm2 = {rm, rm};
 #pragma unroll
     for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;   // f16(S - rm)  (int8:211, 232-236)
@@ -294,248 +331,178 @@ __global__ __launch_bounds__(256, QA_FWD_OCC) void int8_attn_fwd_kernel(
         for (int e = 0; e < 2; ++e)
           if (acc[2 * j + e] == INT_MIN) st.d[j][e] = ninf;
     }
-    return rm;
-  };
-  auto sm1b = [&](_Float16 rm, SmTile& st) {
     if (__ballot((float)rm > (float)m + C::THR) != 0) {
+      // (the empty volatile asm keeps this rare branch a branch: if-converted, the O rescale costs
+      // 2 * D / 2 packed multiplies on every tile)
+      asm volatile("" ::: "memory");
       const _Float16 nm = m > rm ? m : rm;
       const float r = exp2_f32((float)(_Float16)(m - nm));
       m = nm;
       l *= r;
+      if constexpr (PV == PV_I8) obias *= r;
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b) o[b] *= r;
     }
     st.er = exp2_f32((float)(_Float16)(rm - m));
-    st.sp = (_Float16)(st.er * (1.0f / 127.0f));
+    if constexpr (PV == PV_F16) st.cpv = (float)(_Float16)(st.er * (1.0f / 127.0f));
+    else st.cpv = st.er * svq_lds[t];
   };
 
-  // second half: e = exp2(d), l += er * sum e, P operand (2 x 8 packed pairs = 2 x v8h)
-  auto sm2 = [&](const SmTile& st, v4u* pw) {
-    const v2h one2 = {(_Float16)1.0f, (_Float16)1.0f};
-    v2h e[8], w[8];
+  // second half: e = exp2(d) (sm2_exp), then l += er * sum e and the P operand (sm2)
+  //   PV_F16: f16(P_i8 * sp) as 2 x 4 packed dwords; PV_I8: the 16 P_i8 bytes
+  auto sm2_exp = [&](const SmTile& st, v2h* e) {
     exp2_pk4(&st.d[0], &e[0]);
     exp2_pk4(&st.d[4], &e[4]);
-    // row-sum of e: one packed f16 add level (pairs of values <= 1), then fp32; v_dot2c_f32_f16 is
-    // avoided: beside MFMAs it issues ~5x slower than plain VALU (tools/ubench)
-    float esum;   // (not 0.f + ...: a float +0 is not folded away)
-    {
-      const v2h p = e[0] + e[1];
-      esum = (float)p[0] + (float)p[1];
-    }
+  };
+  auto sm2 = [&](const SmTile& st, const v2h* e, v4u* pw) {
+    // row sum of e: packed f16 adds (pairs, then sums of 4 and 8 values <= 8), one f32 mix-add
+    const v2h s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+    l = fmaf(pk_hsum(s), st.er, l);
+    if constexpr (PV == PV_F16) {
+      const _Float16 sp = (_Float16)st.cpv;
+      const v2h sp2 = {sp, sp};
+      const _Float16 nsp = (_Float16)(-1024.0f) * sp;
+      const v2h nsp2 = {nsp, nsp};
+      v2h w[8];
+      p_operand8(e, sp2, nsp2, w);
 #pragma unroll
-    for (int j = 1; j < 4; ++j) {
-      const v2h p = e[2 * j] + e[2 * j + 1];
-      esum += (float)p[0] + (float)p[1];
-    }
-    (void)one2;
-    l += esum * st.er;
-    const v2h sp2 = {st.sp, st.sp};
-    const _Float16 nsp = (_Float16)(-1024.0f) * st.sp;
-    const v2h nsp2 = {nsp, nsp};
-#ifdef QA_FWD_PTRUNC
-    {
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pw[u][j] = __builtin_bit_cast(unsigned, w[4 * u + j]);
+    } else {
       const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
-      v2h x[8], t[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = e[j] * k127;
-      trunc_pk4(&x[0], &t[0]);
-      trunc_pk4(&x[4], &t[4]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) w[j] = t[j] * sp2;
-      (void)nsp2;
+      unsigned y[8];
+      p_index8(e, k127, y);
+      pw[0] = __builtin_bit_cast(v4u, pack_p_index(y));
     }
-#else
-    p_operand8(e, sp2, nsp2, w);
-#endif
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pw[s][j] = __builtin_bit_cast(unsigned, w[4 * s + j]);
   };
 
-  // O^T += Vdq^T P^T for tile t: operand loads (issued early, consumed after QK(t+1) and SM2(t))
+  // O^T += V^T P^T for tile t: operand loads (issued early, consumed after QK(t+1) and SM2(t))
   // and the MFMAs
-  auto pv_load = [&](auto t, v8h* va) {
+  using VFrag = typename std::conditional<PV == PV_F16, v8h, v4i>::type;
+  constexpr int NVF = PV == PV_F16 ? 2 * C::NDB : C::NDB;
+  auto pv_load = [&](int t, VFrag* va) {
     const char* vl = slot_of(t);
+    if constexpr (PV == PV_F16) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int b = 0; b < C::NDB; ++b) {
-        const char* a = vl + voff[b] + 16 * s * 2 * D;
-        if (AB == 6 && s == 1) { va[s * C::NDB + b] = va[b] * (_Float16)2.0f; continue; }   // half the V reads (timing)
-        va[s * C::NDB + b] = __builtin_bit_cast(v8h, ds_read_tr16_x2(a, a + 8 * 2 * D));
-      }
-  };
-  auto pv_mma = [&](const v8h* va, const v4u* pw) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int b = 0; b < C::NDB; ++b) {
-        if constexpr (AB == 2) {
-          asm volatile("" ::"v"(va[s * C::NDB + b]), "v"(pw[s]));
-        } else {
-          o[b] = mfma_f16(va[s * C::NDB + b], __builtin_bit_cast(v8h, pw[s]), o[b]);
+        for (int b = 0; b < C::NDB; ++b) {
+          const char* a = vl + voff[b] + 16 * s * 2 * D;
+          va[s * C::NDB + b] = __builtin_bit_cast(v8h, ds_read_tr16_x2(a, a + 8 * 2 * D));
         }
-      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < C::NDB; ++b) va[b] = *reinterpret_cast<const v4i*>(vl + voff[b]);
+    }
+  };
+  v16i pacc[PV == PV_I8 ? C::NDB : 1];
+  auto pv_mma = [&](const VFrag* va, const v4u* pw) {
+    if constexpr (PV == PV_F16) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int b = 0; b < C::NDB; ++b)
+          o[b] = mfma_f16(va[s * C::NDB + b], __builtin_bit_cast(v8h, pw[s]), o[b]);
+    } else {
+      const v4i p = __builtin_bit_cast(v4i, pw[0]);
+#pragma unroll
+      for (int b = 0; b < C::NDB; ++b) pacc[b] = mfma_i8(va[b], p, kmag);
+    }
+  };
+  // PV_I8: O += (KMAG + X) * (sp * sv) for the tile's exact int32 X (one fused op per element)
+  auto pv_dequant = [&](float cpv) {
+    if constexpr (PV == PV_I8) {
+#pragma unroll
+      for (int b = 0; b < C::NDB; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[b][r] = fmaf(__int_as_float(pacc[b][r]), cpv, o[b][r]);
+      obias += cpv;
+    }
   };
 
-#if defined(QA_FWD_PRIO)
-  {  // co-resident workgroups (blocks b, b+256, b+512 on one CU in the first wave of dispatch) get
-     // different static priorities so that their identical streams do not run in lockstep
-    const int pr = (blockIdx.x >> 8) % 3;
-    if (pr == 1) __builtin_amdgcn_s_setprio(1);
-    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-  }
-#endif
-#if defined(QA_FWD_SLEEP)
-  {
-    const int pr = (blockIdx.x >> 8) % 3;
-    if (pr == 1) __builtin_amdgcn_s_sleep(QA_FWD_SLEEP);
-    else if (pr == 2) { __builtin_amdgcn_s_sleep(QA_FWD_SLEEP); __builtin_amdgcn_s_sleep(QA_FWD_SLEEP); }
-  }
-#endif
   vmem_drain();
   __syncthreads();
 
   SmTile st;
   if (active) {
-    const v16i acc0 = qk(0);
-    if constexpr (SOFTMAX) sm1b(sm1a(acc0, cq * (float)sk_lds[0], st, 0), st);
-    else st.d[0] = __builtin_bit_cast(v2h, acc0[0]);
+    v4i kf[C::NKS];
+    qk_load(0, kf);
+    sm1(qk_mma(kf), 0, st);
   }
   // Steady state: one basic block per tile (except the rare running-max rescale).  The last
   // iteration computes QK / SM1 of a duplicate of the last tile (its slot holds a clamped re-load):
   // harmless (its row max cannot move m) and it keeps the loop body branch-free.
-#if defined(QA_FWD_STAMP)
-  unsigned long long wg_t0 = __builtin_amdgcn_s_memtime();
-  // timing build: per-phase s_memtime stamps of workgroups 0..31, tiles 0..63
-  unsigned long long* stamp = g_fwd_stamps + ((long)(blockIdx.x * C::WAVES + wave) * 64) * 8;
-  const bool do_stamp = blockIdx.x < 32;
-#define QA_STAMP(k)                                                                  \
-  if (do_stamp && t < 64 && lane == 0) {                                             \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-    stamp[t * 8 + (k)] = __builtin_amdgcn_s_memtime();                               \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-  }
-#else
-#define QA_STAMP(k)
-#endif
-  // one tile: SLc holds tile t, NXc tile t+1 (the slot after the last one holds a clamped duplicate),
-  // DMc is the slot the DMA of tile t+3 refills
-  auto step = [&](auto SLc, auto NXc, auto DMc, int t) {
-    QA_STAMP(0)
-    if constexpr (STREAM) {
-#if defined(QA_FWD_NOBAR)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::IPW) : "memory");   // timing experiment only
-#else
-      ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
-#endif
-      QA_STAMP(1)
-      dma.issue(smem_lds + slot_idx(DMc) * C::SLOT, min(t + 3, nt - 1));
-    }
+  for (int t = 0; t < nt; ++t) {
+    ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
+    dma.issue(smem_lds + ((t + 3) & (C::NSLOT - 1)) * C::SLOT, min(t + 3, nt - 1));
     if (active) {
+      // Phase order (pinned: hipcc otherwise issues the QK(t+1) chain right before its consumer
+      // SM1(t+1) and the wave stalls on it): fragment reads, the 16 exponentials of tile t (which
+      // cover the LDS latency), QK(t+1), then the rest of SM2(t), PV(t) and SM1(t+1).
       const int tn = min(t + 1, nt - 1);
-      const float cn = cq * (float)sk_lds[tn];
       v4i kf[C::NKS];
-      qk_load(NXc, kf);
-      v8h va[2 * C::NDB];
-#if defined(QA_FWD_VLATE)
-      // the V reads join the LDS queue only after this wave's K reads have returned, so the K reads
-      // of the other waves of the workgroup (all released by the same barrier) are not queued
-      // behind 4 x 16 transposed V reads
+      qk_load(tn, kf);
+      VFrag va[NVF];
+      pv_load(t, va);
+      v2h e[8];
+      sm2_exp(st, e);
+      __builtin_amdgcn_sched_barrier(0);
       const v16i nacc = qk_mma(kf);
       __builtin_amdgcn_sched_barrier(0);
-      pv_load(SLc, va);
-      __builtin_amdgcn_sched_barrier(0);
-#else
-      pv_load(SLc, va);
-#endif
-#if defined(QA_FWD_SB)
-      __builtin_amdgcn_sched_barrier(0);   // LDS reads issue first; the softmax VALU covers their latency
       v4u pw[2];
-      sm2(st, pw);
-      __builtin_amdgcn_sched_barrier(0);
-      const v16i nacc = qk_mma(kf);
-#elif !defined(QA_FWD_VLATE)
-      const v16i nacc = qk_mma(kf);
-#endif
-      QA_STAMP(2)
-#if !defined(QA_FWD_SB)
-      v4u pw[2];
-      if constexpr (SOFTMAX) {
-        sm2(st, pw);
-      } else {
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pw[s][j] = __builtin_bit_cast(unsigned, st.d[4 * s + j]) & 0x3fff3fffu;
-      }
-#endif
-      QA_STAMP(3)
+      sm2(st, e, pw);
+      const float cpv = st.cpv;
       pv_mma(va, pw);
-      QA_STAMP(4)
-      if constexpr (SOFTMAX) {
-        const _Float16 rm = sm1a(nacc, cn, st, tn);
-        QA_STAMP(5)
-        sm1b(rm, st);
-      } else {
-        st.d[0] = __builtin_bit_cast(v2h, nacc[0]);
-      }
-      QA_STAMP(6)
+      sm1(nacc, tn, st);
+      pv_dequant(cpv);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
     }
-    };
-#if QA_FWD_UNROLL
-  static_assert(C::NSLOT == 4, "unrolled for the 4-slot ring");
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  for (int t = 0; t < nt; t += 4) {
-    step(I0{}, I1{}, I3{}, t);
-    if (t + 1 < nt) step(I1{}, I2{}, I0{}, t + 1);
-    if (t + 2 < nt) step(I2{}, I3{}, I1{}, t + 2);
-    if (t + 3 < nt) step(I3{}, I0{}, I2{}, t + 3);
   }
-#else
-  for (int t = 0; t < nt; ++t) step(t, t + 1, t + 3, t);
-#endif
-#undef QA_STAMP
-  if constexpr (STREAM) vmcnt_wait_all();
+  vmcnt_wait_all();
   __syncthreads();   // every wave is done with the ring: its slots become the output staging area
 
   if (!active) return;
-#if defined(QA_FWD_STAMP)
-  if (tid == 0 && blockIdx.x < 8192) {   // per workgroup: start, end, HW_ID, XCC_ID
-    unsigned long long* w = g_fwd_wginfo + 4L * blockIdx.x;
-    w[0] = wg_t0;
-    w[1] = __builtin_amdgcn_s_memtime();
-    w[2] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID, 32 bits
-    w[3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // HW_REG_XCC_ID
-  }
-#endif
   // ---------------- epilogue: lse = fp16(m + fp16(log2 l)); O = fp16(O / l)   (int8:252-257)
   l = pair_sum(l);
   const long qrow = head_row0 + q0 + c32;
   if (h == 0) lse[qrow] = (_Float16)((float)m + (float)(_Float16)log2_f32(l));
-  static_assert(C::WAVES * RowTile<D, _Float16>::BYTES <= C::NSLOT * C::SLOT, "staging fits the ring");
-  store_rows<D, _Float16>(o, 1.0f / l, smem + wave * RowTile<D, _Float16>::BYTES,
-                          out + (head_row0 + q0) * D, lane);
+  const float inv = 1.0f / l;
+  store_rows<D, _Float16, 1, PV == PV_I8>(o, inv, smem + wave * RowTile<D, _Float16>::BYTES,
+                                          out + (head_row0 + q0) * D, lane, -KMAG * obias * inv);
 }
 
-template <int D, int AB, bool CAUSAL>
+template <int D, int PV, bool CAUSAL>
 static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                      const void* vdq, void* out, void* lse, long bh, long sq_tok, long sk_tok, int group,
-                      float qks, hipStream_t st) {
-  using C = Int8FwdCfg<D>;
+                      const void* vop, const void* sv, void* out, void* lse, long bh, long sq_tok,
+                      long sk_tok, int group, int qoff, float qks, hipStream_t st) {
+  using C = Int8FwdCfg<D, PV>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
-  const int lds = C::NSLOT * C::SLOT + (int)(((sk_tok / 32) * 2 + 15) / 16 * 16);
-  hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<D, AB, CAUSAL>,
+  const int lds = C::RING + (int)(((sk_tok / 32) * 4 * (PV == PV_I8 ? 2 : 1) + 15) / 16 * 16);
+  hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<D, PV, CAUSAL>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((int8_attn_fwd_kernel<D, AB, CAUSAL>), dim3((unsigned)(nq * bh)),
+  hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV, CAUSAL>), dim3((unsigned)(nq * bh)),
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
-                     (const int8_t*)k_i8, (const _Float16*)sk, (const _Float16*)vdq, (_Float16*)out,
-                     (_Float16*)lse, (int)bh, (int)sq_tok, (int)sk_tok, group, qks);
+                     (const int8_t*)k_i8, (const _Float16*)sk, vop, (const _Float16*)sv,
+                     (_Float16*)out, (_Float16*)lse, (int)bh, (int)sq_tok, (int)sk_tok, group, qoff, qks);
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+template <int PV>
+static int fwd_dispatch(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
+                        const void* vop, const void* sv, void* out, void* lse, long bh, long sq_tok,
+                        long sk_tok, int group, int causal, int head_dim, float qks, void* stream) {
+  if (sq_tok % 32 != 0 || sk_tok % 32 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128) || causal < 0 || causal > 2)
+    return 1;
+  if (bh == 0 || sq_tok == 0) return 0;
+  if (sk_tok == 0 || (causal == 2 && sk_tok < sq_tok)) return 1;   // every query keeps a key
+  const int qoff = causal == 2 ? (int)(sk_tok - sq_tok) : 0;
+  hipStream_t st = (hipStream_t)stream;
+#define QA_L(Dv, CV) \
+  launch_fwd<Dv, PV, CV>(q_i8, sq, k_i8, sk, vop, sv, out, lse, bh, sq_tok, sk_tok, group, qoff, qks, st)
+  if (head_dim == 128) return causal ? QA_L(128, true) : QA_L(128, false);
+  return causal ? QA_L(64, true) : QA_L(64, false);
+#undef QA_L
 }
 
 }  // namespace qattn
@@ -546,16 +513,8 @@ extern "C" int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const vo
                                       const void* sk, const void* vdq, void* out, void* lse, long bh,
                                       long sq_tok, long sk_tok, int group, int causal, int head_dim,
                                       float qks, void* stream) {
-  if (sq_tok % 32 != 0 || sk_tok % 32 != 0 || group < 1 || bh % group != 0 ||
-      (head_dim != 64 && head_dim != 128))
-    return 1;
-  if (bh == 0 || sq_tok == 0) return 0;
-  if (sk_tok == 0) return 1;
-  hipStream_t st = (hipStream_t)stream;
-#define QA_L(Dv, CV) launch_fwd<Dv, 0, CV>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, sq_tok, sk_tok, group, qks, st)
-  if (head_dim == 128) return causal ? QA_L(128, true) : QA_L(128, false);
-  return causal ? QA_L(64, true) : QA_L(64, false);
-#undef QA_L
+  return fwd_dispatch<PV_F16>(q_i8, sq, k_i8, sk, vdq, nullptr, out, lse, bh, sq_tok, sk_tok, group,
+                              causal, head_dim, qks, stream);
 }
 
 extern "C" int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
@@ -565,27 +524,11 @@ extern "C" int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void*
                                 stream);
 }
 
-extern "C" int qattn_int8_attn_fwd_ablate(const void* q_i8, const void* sq, const void* k_i8,
-                                          const void* sk, const void* vdq, void* out, void* lse,
-                                          long bh, long seq, float qks, int ab, void* stream) {
-  if (seq % 32 != 0 || bh == 0) return 1;
-  hipStream_t st = (hipStream_t)stream;
-  switch (ab) {
-    case 1: return launch_fwd<128, 1, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
-    case 2: return launch_fwd<128, 2, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
-    case 3: return launch_fwd<128, 3, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
-    case 4: return launch_fwd<128, 4, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
-    case 5: return launch_fwd<128, 5, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
-    case 6: return launch_fwd<128, 6, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
-    case 7: return launch_fwd<128, 7, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
-    default: return launch_fwd<128, 0, false>(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, qks, st);
-  }
+extern "C" int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, const void* k_i8,
+                                           const void* sk, const void* vt, const void* sv, void* out,
+                                           void* lse, long bh, long sq_tok, long sk_tok, int group,
+                                           int causal, int head_dim, float qks, void* stream) {
+  if (sv == nullptr) return 1;
+  return fwd_dispatch<PV_I8>(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, causal,
+                             head_dim, qks, stream);
 }
-
-#if defined(QA_FWD_STAMP)
-extern "C" int qattn_fwd_stamps(void* stamps, void* wginfo) {
-  hipMemcpyFromSymbol(stamps, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps));
-  hipMemcpyFromSymbol(wginfo, HIP_SYMBOL(g_fwd_wginfo), sizeof(g_fwd_wginfo));
-  return 0;
-}
-#endif

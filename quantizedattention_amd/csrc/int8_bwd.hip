@@ -639,6 +639,10 @@ void int8_bwd_kernel(
 #ifndef QA_DQW_NT
 #define QA_DQW_NT 1
 #endif
+// The dK+dV kernel (8 waves) writes records only for q-tiles >= its workgroup's first key tile,
+// and this kernel reads every key tile up to its workgroup's last query tile for all of its waves:
+// with more than 8 waves per workgroup the first ones would read records never written (causal).
+static_assert(QA_DQW_WAVES <= 8, "dQ-from-records workgroups may not exceed the dK+dV kernel's 8 waves");
 template <int D>
 struct DqwCfg {
   static constexpr int WAVES = QA_DQW_WAVES;
@@ -982,8 +986,15 @@ extern "C" int qattn_int8_bwd_dq(const void* dO_i8, const void* sdO, const void*
                          nullptr, nullptr, bh, seq, seq, 1, 0, head_dim, qks, sms, stream);
 }
 
+// The dK+dV kernel addresses the records of one key/value head (its G query heads) with 32-bit
+// buffer offsets: that region, G * (sq/32) * (sk/32) KiB, must stay below 2^31 bytes.
+static bool ws_region_fits(long group, long sq_tok, long sk_tok) {
+  return group * (sq_tok / 32) * (sk_tok / 32) * 1024 < (1L << 31);
+}
+
 extern "C" long qattn_int8_bwd_ws_bytes(long bh, long sq_tok, long sk_tok) {
   if (sq_tok % 32 != 0 || sk_tok % 32 != 0 || bh < 0) return -1;
+  if (!ws_region_fits(1, sq_tok, sk_tok)) return -1;   // too large even ungrouped: recompute instead
   return bh * (sq_tok / 32) * (sk_tok / 32) * (1024 + 4);
 }
 
@@ -994,7 +1005,7 @@ extern "C" int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const 
                                       void* dk, void* dv, void* ws, long bh, long sq_tok, long sk_tok,
                                       int group, int causal, int head_dim, float qks, float sms,
                                       void* stream) {
-  if (ws == nullptr) return 1;
+  if (ws == nullptr || group < 1 || !ws_region_fits(group, sq_tok, sk_tok)) return 1;
   return int8_bwd_launch(16 | 32, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD,
                          q_bf, k_bf, dO_bf, dq, dk, dv, bh, sq_tok, sk_tok, group, causal, head_dim, qks,
                          sms, stream, ws);
@@ -1007,7 +1018,7 @@ extern "C" int qattn_int8_bwd_dkdv_ws(const void* dO_i8, const void* sdO, const 
                                       const void* q_bf, const void* dO_bf, void* dk, void* dv, void* ws,
                                       long bh, long seq, int head_dim, float qks, float sms,
                                       void* stream) {
-  if (ws == nullptr) return 1;
+  if (ws == nullptr || !ws_region_fits(1, seq, seq)) return 1;
   return int8_bwd_launch(16, dO_i8, sdO, q_i8, sq, k_i8, sk, v_i8, sv, LD, q_bf,
                          nullptr, dO_bf, nullptr, dk, dv, bh, seq, seq, 1, 0, head_dim, qks, sms, stream,
                          ws);

@@ -73,6 +73,77 @@ __global__ __launch_bounds__(256) void quant_block32_kernel(
   }
 }
 
+// ------------------------------------------------------------ V with the int8 P.V operand image
+// One wave per 32-row block of v: the reference quantiser (v_i8 row-major + sv, bit-exact as above)
+// and, of the same indices, the V^T operand image vt of the forward's int8 P.V product
+// (qattn_int8_attn_fwd_i8pv_ex): per block D/32 pieces of 1 KiB; piece b holds for lane
+// L = 32h + c the 16 bytes v_i8[key pi(h, j)][32b + c], j = 0..15, pi(h, j) = (j & 3) + 8(j >> 2) + 4h
+// -- the A operand of v_mfma_i32_32x32x32_i8 for V^T in the key order of the S^T accumulator
+// (common.h).  Lane (row c, half h) loads v[c][32b + 16h .. +16]: exactly the A operand of the
+// block in natural order, which one i8 MFMA against the identity transposes into that image.
+QA_DEVICE v4i pack16_i8(const int* q) {
+  v4i a;
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+    a[w] = (q[4 * w] & 0xff) | ((q[4 * w + 1] & 0xff) << 8) | ((q[4 * w + 2] & 0xff) << 16) |
+           (q[4 * w + 3] << 24);
+  return a;
+}
+template <int D>
+__global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restrict__ v,
+                                                       int8_t* __restrict__ vi,
+                                                       _Float16* __restrict__ sv,
+                                                       int8_t* __restrict__ vt, long nblocks) {
+  constexpr int NDB = D / 32;
+  const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= nblocks) return;
+  const long row = blk * 32 + c;
+  v8h x[NDB][2];
+  float amax = 0.f;
+#pragma unroll
+  for (int b = 0; b < NDB; ++b)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      x[b][u] = *reinterpret_cast<const v8h*>(v + row * D + 32 * b + 16 * h + 8 * u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf((float)x[b][u][j]));
+    }
+  amax = wave_max_f(amax);
+  const _Float16 s16 = (_Float16)(amax / 127.0f);
+  const float s = (float)s16;
+  if (lane == 0) sv[blk] = s16;
+  const v4i ident = identity_b_i8(lane);
+#pragma unroll
+  for (int b = 0; b < NDB; ++b) {
+    int q[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      q[j] = s != 0.f ? (int)__builtin_truncf((float)(_Float16)((float)x[b][j >> 3][j & 7] / s)) : 0;
+    const v4i a = pack16_i8(q);
+    *reinterpret_cast<v4i*>(vi + row * D + 32 * b + 16 * h) = a;
+    const v16i t = mfma_i8(a, ident, v16i{});
+    *reinterpret_cast<v4i*>(vt + blk * 32 * D + b * 1024 + 16 * lane) = pack_acc_bytes(t);
+  }
+}
+// vt from stored indices (an int8 key/value cache restored from its wire format, kv_cache.py)
+template <int D>
+__global__ __launch_bounds__(256) void v_image_kernel(const int8_t* __restrict__ vi,
+                                                      int8_t* __restrict__ vt, long nblocks) {
+  constexpr int NDB = D / 32;
+  const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= nblocks) return;
+  const long row = blk * 32 + c;
+  const v4i ident = identity_b_i8(lane);
+#pragma unroll
+  for (int b = 0; b < NDB; ++b) {
+    const v4i a = *reinterpret_cast<const v4i*>(vi + row * D + 32 * b + 16 * h);
+    const v16i t = mfma_i8(a, ident, v16i{});
+    *reinterpret_cast<v4i*>(vt + blk * 32 * D + b * 1024 + 16 * lane) = pack_acc_bytes(t);
+  }
+}
+
 // k_mean[bh][d] = fp16( sum_s fp32(k[bh][s][d]) / S )   (eager `k.mean(-2)` in fp16, fp32 accumulate)
 // One 1024-thread workgroup per head; 4 independent 16-B loads in flight per thread.
 template <int D>
@@ -153,6 +224,35 @@ extern "C" int qattn_int8_quant(const void* x, void* idx, void* scale, void* deq
                                 long rows, int rows_per_head, int head_dim, void* stream) {
   return qattn_int8_quant_img(x, idx, scale, deq, nullptr, kmean, rows, rows_per_head, head_dim,
                               stream);
+}
+
+extern "C" int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt, long rows,
+                                   int head_dim, void* stream) {
+  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  const long nblocks = rows / 32;
+  if (nblocks == 0) return 0;
+  dim3 grid((unsigned)((nblocks + 3) / 4)), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (head_dim == 128)
+    hipLaunchKernelGGL(quant_vt_kernel<128>, grid, block, 0, st, (const _Float16*)v, (int8_t*)v_i8,
+                       (_Float16*)sv, (int8_t*)vt, nblocks);
+  else
+    hipLaunchKernelGGL(quant_vt_kernel<64>, grid, block, 0, st, (const _Float16*)v, (int8_t*)v_i8,
+                       (_Float16*)sv, (int8_t*)vt, nblocks);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_int8_v_image(const void* v_i8, void* vt, long rows, int head_dim, void* stream) {
+  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  const long nblocks = rows / 32;
+  if (nblocks == 0) return 0;
+  dim3 grid((unsigned)((nblocks + 3) / 4)), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (head_dim == 128)
+    hipLaunchKernelGGL(v_image_kernel<128>, grid, block, 0, st, (const int8_t*)v_i8, (int8_t*)vt, nblocks);
+  else
+    hipLaunchKernelGGL(v_image_kernel<64>, grid, block, 0, st, (const int8_t*)v_i8, (int8_t*)vt, nblocks);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 extern "C" int qattn_kmean(const void* k, void* kmean, long bh, long seq, int head_dim, void* stream) {

@@ -20,8 +20,14 @@ Wire format (little-endian, version 1)::
                                                             index (b * kv_heads + h) * tokens / 32 + s / 32
       k_mean  float16 [batch, kv_heads, 1, head_dim]        only when "smoothed" (SageAttention k-smoothing)
 
-The fp16 operand f16(v_i8 * sv) of the P.V product is not stored: :meth:`QuantizedKV.vdq` rebuilds it
-on the GPU (``qattn_int8_dequant``) bit-identically to the quantiser's own output.
+The forward's P.V operand is not stored either: :meth:`QuantizedKV.operand` rebuilds it on the GPU
+from v_i8 (and sv) -- f16(v_i8 * sv) for the f16 P.V mode (``qattn_int8_dequant``), the int8 V^T
+operand image for the int8 mode (``qattn_int8_v_image``) -- bit-identically to the quantisers' own
+outputs.
+
+Causal attention against a cache aligns the LAST query with the LAST key (query i of the Sq new
+ones sits at position Sk - Sq + i and keeps the keys up to it: ``causal = 2`` of
+qattn_int8_attn_fwd_ex), so a decode step sees the whole prefix.
 """
 from __future__ import annotations
 
@@ -56,13 +62,14 @@ class QuantizedKV:
     sv: torch.Tensor
     k_mean: Optional[torch.Tensor] = None
     _vdq: Optional[torch.Tensor] = None
+    _vt: Optional[torch.Tensor] = None
 
     @property
     def shape(self):
         return tuple(self.k_i8.shape)
 
     def vdq(self) -> torch.Tensor:
-        """f16(v_i8 * sv) [B*Hkv*S, D], the forward's P.V operand (rebuilt on demand, cached)."""
+        """f16(v_i8 * sv) [B*Hkv*S, D], the f16-mode P.V operand (rebuilt on demand, cached)."""
         if self._vdq is None:
             B, H, S, D = self.shape
             _lib.require_gpu(self.v_i8, self.sv)
@@ -71,6 +78,21 @@ class QuantizedKV:
                       B * H * S, D, _lib.stream_of(self.v_i8))
             self._vdq = out
         return self._vdq
+
+    def vt(self) -> torch.Tensor:
+        """The int8 V^T operand image of v_i8 [B*Hkv*S, D] bytes, the int8-mode P.V operand."""
+        if self._vt is None:
+            B, H, S, D = self.shape
+            _lib.require_gpu(self.v_i8)
+            out = torch.empty((B * H * S, D), dtype=torch.int8, device=self.v_i8.device)
+            _lib.call("qattn_int8_v_image", _lib.ptr(self.v_i8.contiguous()), _lib.ptr(out), B * H * S, D,
+                      _lib.stream_of(self.v_i8))
+            self._vt = out
+        return self._vt
+
+    def operand(self, pv: str) -> torch.Tensor:
+        """The P.V operand of mode ``pv`` ("f16" or "i8", attention_int8.PV_MODE)."""
+        return self.vdq() if pv == "f16" else self.vt()
 
     # ------------------------------------------------------------------------------ growth
     def append(self, k: torch.Tensor, v: torch.Tensor) -> "QuantizedKV":
@@ -183,15 +205,21 @@ def quantize_kv(k: torch.Tensor, v: torch.Tensor, smooth: bool = True,
     return QuantizedKV(k_i8, v_i8, sk, sv, km, vdq)
 
 
-def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False):
+def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False, pv=None):
     """int8 attention of fp16 queries [B, Hq, Sq, D] against a quantised cache (inference; no autograd).
 
-    Hq must be a multiple of the cache's heads (grouped-query attention).  Returns (O fp16
-    [B, Hq, Sq, D], lse fp16 [B*Hq*Sq]), identical to the forward on the un-cached tensors.
+    Hq must be a multiple of the cache's heads (grouped-query attention).  ``causal``: the Sq queries
+    are the LAST Sq positions (query i keeps keys <= Sk - Sq + i), Sq <= Sk.  Returns (O fp16
+    [B, Hq, Sq, D], lse fp16 [B*Hq*Sq]); without ``causal`` identical to the forward on the un-cached
+    tensors.  ``pv``: the P.V mode (default attention_int8.PV_MODE).
     """
+    from . import attention_int8
+    pv = attention_int8.PV_MODE if pv is None else pv
     B, Hkv, Sk, D = kv.shape
     if q.dim() != 4 or q.shape[0] != B or q.shape[3] != D or q.shape[1] % Hkv or q.shape[2] % BLOCK:
         raise _lib.QAttnError("qattn kv cache: q must be [B, G*Hkv, 32*n, D] for the cache's B, Hkv, D")
+    if causal and q.shape[2] > Sk:
+        raise _lib.QAttnError("qattn kv cache: causal attention needs Sq <= the cached tokens")
     _lib.require_gpu(q, kv.k_i8)
     q = q.to(torch.float16).contiguous()
     Hq, Sq = q.shape[1], q.shape[2]
@@ -203,7 +231,13 @@ def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False
     lse = torch.empty((N,), dtype=torch.float16, device=dev)
     _lib.call("qattn_int8_quant", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), None, None, N, Sq, D, st)
     qks = float(torch.tensor(1.0 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
-    _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8), _lib.ptr(kv.sk),
-              _lib.ptr(kv.vdq()), _lib.ptr(O), _lib.ptr(lse), B * Hq, Sq, Sk, Hq // Hkv,
-              int(bool(causal)), D, qks, st)
+    mode = 2 if causal else 0          # bottom-right aligned causal mask
+    if pv == "f16":
+        _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
+                  _lib.ptr(kv.sk), _lib.ptr(kv.vdq()), _lib.ptr(O), _lib.ptr(lse), B * Hq, Sq, Sk,
+                  Hq // Hkv, mode, D, qks, st)
+    else:
+        _lib.call("qattn_int8_attn_fwd_i8pv_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
+                  _lib.ptr(kv.sk), _lib.ptr(kv.vt()), _lib.ptr(kv.sv), _lib.ptr(O), _lib.ptr(lse),
+                  B * Hq, Sq, Sk, Hq // Hkv, mode, D, qks, st)
     return O, lse

@@ -145,6 +145,14 @@ def test_bwd_workspace_size():
     assert lib.qattn_int8_bwd_ws_bytes(6, 96, 160) == 6 * 3 * 5 * 1028
     assert lib.qattn_int8_bwd_ws_bytes(2, 100, 64) == -1          # tokens not a multiple of 32
     assert lib.qattn_int8_bwd_ws_bytes(0, 64, 64) == 0
+    # one key/value head's records are addressed with 32-bit offsets: (S/32)^2 KiB < 2 GiB
+    assert lib.qattn_int8_bwd_ws_bytes(1, 46336, 46336) > 0          # 1448^2 KiB < 2 GiB
+    assert lib.qattn_int8_bwd_ws_bytes(1, 65536, 65536) == -1         # 4 GiB region: recompute
+    assert lib.qattn_int8_bwd_ws_bytes(8, 32768, 65536) == -1         # 2 GiB region
+    # the grouped check is in the launcher: G = 8 query heads at S = 32768 is 8 GiB per kv head
+    # (a non-null workspace pointer: the guard answers before anything touches memory or a device)
+    assert lib.qattn_int8_attn_bwd_ws(*([None] * 15), ctypes.c_void_p(16), 8, 32768, 32768, 8, 0, 128,
+                                      0.0, 0.0, None) == 1
     assert lib.qattn_bf16_bwd_ws_bytes(4 * 32, 4096, 4096) == 128 * 128 * 128 * 2048
     assert lib.qattn_bf16_bwd_ws_bytes(6, 96, 160) == 6 * 3 * 5 * 2048
     assert lib.qattn_bf16_bwd_ws_bytes(2, 100, 64) == -1

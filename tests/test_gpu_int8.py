@@ -20,8 +20,17 @@ def _inputs(shape, seed=0, scale=1.0):
     return [(torch.randn(shape, generator=g) * scale) for _ in range(3)]
 
 
+@pytest.fixture(params=["f16", "i8"])
+def pv(request, monkeypatch):
+    """Both P.V modes of the forward (f16 operands with the tile scale folded in / int8 MFMA with a
+    per-tile dequantisation): same P_i8 and scales, same tolerance."""
+    from quantizedattention_amd import attention_int8
+    monkeypatch.setattr(attention_int8, "PV_MODE", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("shape", SHAPES)
-def test_int8_fwd_matches_oracle(lib, shape):
+def test_int8_fwd_matches_oracle(lib, shape, pv):
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
     q, k, v = _inputs(shape)
     qh, kh, vh = q.half(), k.half(), v.half()
@@ -56,7 +65,7 @@ def test_int8_quant_edge_cases(lib):
     assert torch.equal(out[5].cpu(), ref[5])
 
 
-def test_int8_fwd_deterministic(lib):
+def test_int8_fwd_deterministic(lib, pv):
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
     q, k, v = [t.half().cuda() for t in _inputs((1, 4, 256, 128), seed=3)]
     a = helion_atten_int8_hl_dot_fwd(q, k, v)
@@ -64,7 +73,7 @@ def test_int8_fwd_deterministic(lib):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
-def test_int8_fwd_large_size_properties(lib):
+def test_int8_fwd_large_size_properties(lib, pv):
     """North-star size (4,32,4096,128): finite; constant V reproduces the constant; one head
     checked against the oracle at full length."""
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd

@@ -43,21 +43,61 @@ def _fp16(shape, seed):
     return torch.randn(shape, generator=torch.Generator().manual_seed(seed)).half()
 
 
+@pytest.fixture(params=["f16", "i8"])
+def pv(request, monkeypatch):
+    from quantizedattention_amd import attention_int8
+    monkeypatch.setattr(attention_int8, "PV_MODE", request.param)
+    return request.param
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("hq,hkv,causal", [(4, 4, False), (4, 2, True), (8, 1, False)])
-def test_cached_attention_matches_forward(lib, hq, hkv, causal):
+@pytest.mark.parametrize("hq,hkv", [(4, 4), (4, 2), (8, 1)])
+def test_cached_attention_matches_forward(lib, hq, hkv, pv):
+    """Non-causal: the cached forward through the wire format is bit-identical to the forward on the
+    un-cached tensors (same quantiser, same kernel)."""
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
     from quantizedattention_amd.kv_cache import attention_int8_cached, quantize_kv
     q = _fp16((1, hq, 96, 128), 1).cuda()
     k = _fp16((1, hkv, 160, 128), 2).cuda()
     v = _fp16((1, hkv, 160, 128), 3).cuda()
-    ref = helion_atten_int8_hl_dot_fwd(q, k, v, causal=causal)
+    ref = helion_atten_int8_hl_dot_fwd(q, k, v)
     kv = quantize_kv(k, v, smooth=False)
     kv2 = QuantizedKV.from_bytes(kv.to_bytes().cpu(), device="cuda")   # through the wire format
-    O, lse = attention_int8_cached(q, kv2, causal=causal)
+    O, lse = attention_int8_cached(q, kv2)
     torch.cuda.synchronize()
     assert torch.equal(O, ref[0]) and torch.equal(lse, ref[1])
     assert torch.equal(kv2.k_i8.view(-1, 128), ref[3].t()) and torch.equal(kv2.sk, ref[6])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("sq", [32, 64])
+def test_cached_decode_vs_oracle(lib, causal, sq, pv):
+    """SURVEY §8f N3 against the oracle: a cache grown by append (128 + 32 tokens), moved through
+    to_bytes / from_bytes, attended by Sq new queries; causal aligns the last query with the last key
+    (query i keeps keys <= Sk - Sq + i: the decode step sees the whole prefix).  O within the int8
+    bar (1e-2) and lse within 2 fp16 ulp of oracle/restate.py int8_fwd on the same fp16 inputs
+    (same quantised operands: quantisation is per 32-token block)."""
+    from oracle import restate as R
+    from quantizedattention_amd.kv_cache import attention_int8_cached, quantize_kv
+    hq, hkv, Sk, D = 4, 2, 160, 128
+    q = _fp16((1, hq, sq, D), 11)
+    k = _fp16((1, hkv, Sk, D), 12)
+    v = _fp16((1, hkv, Sk, D), 13)
+    kv = quantize_kv(k[:, :, :128].cuda(), v[:, :, :128].cuda(), smooth=False)
+    kv = kv.append(k[:, :, 128:].cuda(), v[:, :, 128:].cuda())
+    kv = QuantizedKV.from_bytes(kv.to_bytes().cpu(), device="cuda")
+    O, lse = attention_int8_cached(q.cuda(), kv, causal=causal)
+    torch.cuda.synchronize()
+    ref = R.int8_fwd(q, k, v, causal=causal, causal_offset=Sk - sq)
+    assert torch.equal(kv.k_i8.cpu().view(-1, D), ref[3].t()) and torch.equal(kv.v_i8.cpu().view(-1, D), ref[4])
+    err = (O.float().cpu() - ref[0].float()).abs().max().item()
+    assert err <= 1e-2, err
+    lerr = (lse.float().cpu() - ref[1].float()).abs()
+    assert (lerr <= 2 * 2.0 ** -10 * ref[1].float().abs() + 1e-3).all(), lerr.max().item()
+    if causal:   # the last query keeps every key: its row equals the non-causal one bit for bit
+        On, _ = attention_int8_cached(q.cuda(), kv, causal=False)
+        assert torch.equal(O[:, :, -1], On[:, :, -1])
 
 
 @pytest.mark.gpu
@@ -70,16 +110,25 @@ def test_cache_append_and_vdq(lib):
     grown = quantize_kv(k[:, :, :64], v[:, :, :64], smooth=False).append(k[:, :, 64:], v[:, :, 64:])
     for name in ("k_i8", "v_i8", "sk", "sv"):
         assert torch.equal(getattr(grown, name), getattr(whole, name)), name
-    # rebuilt f16(v_i8 * sv) == the quantiser's own deq output
+    # rebuilt f16(v_i8 * sv) == the quantiser's own deq output; rebuilt int8 V^T image == the
+    # int8-mode quantiser's own image
     restored = QuantizedKV.from_bytes(whole.to_bytes())
     assert restored._vdq is None
     assert torch.equal(restored.vdq(), whole.vdq())
+    N = 2 * 2 * 128
+    vi = torch.empty((N, 64), dtype=torch.int8, device="cuda")
+    svv = torch.empty((N // 32,), dtype=torch.float16, device="cuda")
+    vt = torch.empty((N, 64), dtype=torch.int8, device="cuda")
+    _lib.call("qattn_int8_quant_vt", _lib.ptr(v), _lib.ptr(vi), _lib.ptr(svv), _lib.ptr(vt), N, 64,
+              _lib.stream_of(v))
+    assert torch.equal(vi.view(2, 2, 128, 64), whole.v_i8) and torch.equal(svv, whole.sv)
+    assert torch.equal(restored.vt(), vt)
     with pytest.raises(_lib.QAttnError):
         whole.append(k[:, :, :16], v[:, :, :16])
 
 
 @pytest.mark.gpu
-def test_cache_from_forward_outputs(lib):
+def test_cache_from_forward_outputs(lib, pv):
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
     from quantizedattention_amd.kv_cache import attention_int8_cached
     q = _fp16((2, 2, 64, 64), 6).cuda()

@@ -9,6 +9,6 @@ mkdir -p $R/_ab/obj
 OBJ=$R/_ab/obj/$(basename $SRC .hip)_$NAME.o
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt \
   -fno-gpu-rdc -Wno-unused-result -Wno-unused-value -I$R/include "$@" -c $R/quantizedattention_amd/csrc/$SRC -o $OBJ
-OTHERS=$(ls $R/quantizedattention_amd/_build/*.o | grep -v "/$(basename $SRC .hip).o")
+OTHERS=$(ls $R/quantizedattention_amd/_build/*.o | grep -v "/dev_" | grep -v "/$(basename $SRC .hip).o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/_ab/libqattn_$NAME.so $OTHERS $OBJ
 echo "built _ab/libqattn_$NAME.so"

@@ -6,6 +6,6 @@ for v in "$@"; do
   if [ "$v" = default ]; then
     timeout -k 10 90 python "$S" || exit 1
   else
-    QATTN_LIB=_ab/libqattn_$v.so timeout -k 10 90 python "$S" || exit 1
+    QATTN_AB=$PWD/_ab/libqattn_$v.so timeout -k 10 90 python "$S" || exit 1
   fi
 done

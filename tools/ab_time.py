@@ -1,40 +1,81 @@
-"""Time the int8 attention forward kernel of the library named by QATTN_LIB (A/B dev tool)."""
+"""Time the int8 attention forward kernels (both P.V modes) of one library (A/B dev tool:
+tools/ab_build.sh builds variants, tools/ab_run.sh runs this over them).
+
+    QATTN_AB=_ab/libqattn_<variant>.so python tools/ab_time.py [B,H,S,D] [causal]
+
+Exactly ONE library is loaded per process (the variant, or the in-tree build): two copies of the
+same kernels in one process bind each other's identically named template kernel stubs (ELF symbol
+interposition), so a variant would launch the other library's code.  The library is bound here with
+ctypes directly; entries a variant lacks (an older kernel) are skipped."""
+import ctypes
 import math
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from quantizedattention_amd import _lib  # noqa: E402
-from quantizedattention_amd.attention_int8 import _int8_forward  # noqa: E402
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from quantizedattention_amd._lib import SIGNATURES  # noqa: E402  (argtypes only; loads nothing)
+
+path = os.environ.get("QATTN_AB") or os.path.join(ROOT, "quantizedattention_amd", "libqattn.so")
+torch.cuda.init()
+lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def entry(name):
+    fn = getattr(lib, name, None)
+    if fn is not None:
+        fn.argtypes = SIGNATURES[name]
+        fn.restype = ctypes.c_int
+    return fn
+
+
+def call(name, *args):
+    rc = entry(name)(*args)
+    assert rc == 0, (name, rc)
+
 
 B, H, S, D = (int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4,32,4096,128").split(","))
+causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn((B, H, S, D), device="cuda", generator=g).half() for _ in range(3))
-O, lse, qi, kiT, vi, sq, sk, sv, _, _, _ = _int8_forward(q, k, v, False)
 N = B * H * S
-vdq = torch.empty((N, D), dtype=torch.float16, device="cuda")
-st = _lib.stream_of(q)
-P = _lib.ptr
-_lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
-ki = kiT.t()
+st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+e = lambda *s, dt: torch.empty(s, dtype=dt, device="cuda")  # noqa: E731
+qi, ki, vi = (e(N, D, dt=torch.int8) for _ in range(3))
+sq, sk, sv = (e(N // 32, dt=torch.float16) for _ in range(3))
+vdq, vt = e(N, D, dt=torch.float16), e(N, D, dt=torch.int8)
+O, lse = e(N, D, dt=torch.float16), e(N, dt=torch.float16)
+call("qattn_int8_quant", P(q), P(qi), P(sq), None, None, N, S, D, st)
+call("qattn_int8_quant", P(k), P(ki), P(sk), None, None, N, S, D, st)
+call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
+if entry("qattn_int8_quant_vt") is not None:
+    call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
-f = lambda: _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse),  # noqa
-                      B * H, S, D, qks, st)
-for _ in range(3):
-    f()
-torch.cuda.synchronize()
-ts = []
-for _ in range(15):
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    f()
-    b.record()
+fns = {}
+if entry("qattn_int8_attn_fwd_ex") is not None:
+    fns["f16"] = lambda: call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse),
+                              B * H, S, S, 1, int(causal), D, qks, st)
+if entry("qattn_int8_attn_fwd_i8pv_ex") is not None:
+    fns["i8"] = lambda: call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv),
+                             P(O), P(lse), B * H, S, S, 1, int(causal), D, qks, st)
+ops = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
+name = os.path.basename(path)
+for mode, f in fns.items():
+    for _ in range(3):
+        f()
     torch.cuda.synchronize()
-    ts.append(a.elapsed_time(b))
-ts.sort()
-t = ts[len(ts) // 2]
-ops = 4 * B * H * S * S * D
-print(f"{os.environ.get('QATTN_LIB', 'default')}: {t * 1e3:.1f} us  {ops / t / 1e9:.0f} TOPS "
-      f"({ops / t / 1e9 / 5033 * 100:.1f}% i8 peak)", flush=True)
+    ts = []
+    for _ in range(15):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        f()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    t = ts[len(ts) // 2]
+    print(f"{name} pv={mode}{' causal' if causal else ''}: {t * 1e3:.1f} us  {ops / t / 1e9:.0f} TOPS "
+          f"({ops / t / 1e9 / 5033 * 100:.1f}% i8 peak)", flush=True)
