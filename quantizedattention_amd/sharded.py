@@ -69,18 +69,38 @@ def all_gather_bh(local: torch.Tensor, out: torch.Tensor | None = None, group=No
     return out, work
 
 
+def kv_shard(shard: Shard, heads: int, kv_heads: int) -> Shard:
+    """The key/value heads a query-head shard reads under grouped-query attention (query head h of
+    batch b reads key/value head h // G, G = heads / kv_heads): in the flattened views the key/value
+    row of query row i is i // G, so the shard's key/value range is [bh0 / G, bh1 / G).  Raises unless
+    the shard holds whole groups (both bounds multiples of G)."""
+    if heads % kv_heads:
+        raise ValueError(f"query heads {heads} are not a multiple of key/value heads {kv_heads}")
+    G = heads // kv_heads
+    if shard.bh0 % G or shard.bh1 % G:
+        raise ValueError(f"shard [{shard.bh0}, {shard.bh1}) splits a group of {G} query heads that "
+                         "share a key/value head")
+    return Shard(shard.world, shard.rank, shard.bh0 // G, shard.bh1 // G)
+
+
 def sharded_forward(fn, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, group=None,
                     gather: bool = True):
     """Run ``fn(q_loc, k_loc, v_loc) -> O_loc (or a tuple whose [0] is O)`` on this rank's slice of
-    full [B, H, S, D] inputs and (optionally) all-gather O to every rank.
+    full [B, H, S, D] inputs and (optionally) all-gather O to every rank.  k and v may have fewer
+    heads (grouped-query attention): each rank gets the key/value heads its query heads read
+    (:func:`kv_shard`), as [1, n / G, Sk, D].
 
     Returns (O_full or O_local as [B', H', S, D], the raw local result of ``fn``).
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     B, H, S, D = q.shape
+    if k.shape[0] != B or v.shape[:2] != k.shape[:2]:
+        raise ValueError("sharded_forward: k and v need q's batch and one head count")
     sh = shard_for(B, H, world, rank)
-    ql, kl, vl = (local_slice(t, sh).unsqueeze(0) for t in (q, k, v))
+    kvs = kv_shard(sh, H, k.shape[1])
+    ql = local_slice(q, sh).unsqueeze(0)
+    kl, vl = (local_slice(t, kvs).unsqueeze(0) for t in (k, v))
     res = fn(ql.contiguous(), kl.contiguous(), vl.contiguous())
     O_loc = res[0] if isinstance(res, tuple) else res
     if not gather or world == 1:

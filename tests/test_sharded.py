@@ -11,7 +11,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from quantizedattention_amd.sharded import Shard, all_gather_bh, local_slice, shard_for, sharded_forward
+from quantizedattention_amd.sharded import (Shard, all_gather_bh, kv_shard, local_slice, shard_for,
+                                            sharded_forward)
 
 
 @pytest.mark.parametrize("B,H,world", [(4, 32, 1), (4, 32, 2), (4, 32, 8), (8, 32, 8), (1, 16, 4),
@@ -37,6 +38,28 @@ def test_shard_rejects_uneven():
         shard_for(2, 2, 2, 2)
 
 
+@pytest.mark.parametrize("B,H,Hkv,world", [(2, 8, 2, 2), (1, 8, 4, 2), (4, 32, 8, 8), (8, 32, 1, 8)])
+def test_kv_shard_pairs_query_heads_with_their_kv_heads(B, H, Hkv, world):
+    """Grouped-query sharding: every query head of a rank finds its key/value head (h // G within its
+    batch) inside the rank's key/value range."""
+    G = H // Hkv
+    for r in range(world):
+        s = shard_for(B, H, world, r)
+        kvs = kv_shard(s, H, Hkv)
+        for i in range(s.bh0, s.bh1):
+            b, h = divmod(i, H)
+            kv_flat = b * Hkv + h // G
+            assert kvs.bh0 <= kv_flat < kvs.bh1
+            assert kv_flat - kvs.bh0 == (i - s.bh0) // G
+
+
+def test_kv_shard_rejects_split_groups():
+    assert kv_shard(shard_for(1, 6, 2, 0), 6, 2) == Shard(2, 0, 0, 1)   # 3 query heads = 1 group
+    # H = 4, Hkv = 1 (G = 4) over 2 ranks of 2 query heads each: every rank splits the group
+    with pytest.raises(ValueError, match="splits a group"):
+        kv_shard(shard_for(1, 4, 2, 0), 4, 1)
+
+
 def test_local_slice_is_view():
     x = torch.randn(2, 4, 8, 16)
     s = Shard(2, 1, 4, 8)
@@ -50,18 +73,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, B, H, S, D, errq):
+def _worker(rank, world, port, B, H, S, D, errq, Hkv=None):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from oracle import restate as R
         g = torch.Generator().manual_seed(11)
-        q, k, v = (torch.randn((B, H, S, D), generator=g) for _ in range(3))
-        full = R.baseline_pytorch_attention(q, k, v)
+        Hk = H if Hkv is None else Hkv
+        q = torch.randn((B, H, S, D), generator=g)
+        k, v = (torch.randn((B, Hk, S, D), generator=g) for _ in range(2))
+        rep = lambda t: t.repeat_interleave(H // Hk, dim=1)  # noqa: E731
+        full = R.baseline_pytorch_attention(q, rep(k), rep(v))
 
-        def fn(ql, kl, vl):
-            return R.baseline_pytorch_attention(ql, kl, vl), None
+        def fn(ql, kl, vl):   # grouped-query attention on the local heads
+            G = ql.shape[1] // kl.shape[1]
+            return R.baseline_pytorch_attention(ql, kl.repeat_interleave(G, 1), vl.repeat_interleave(G, 1)), None
 
         O, res = sharded_forward(fn, q, k, v)
         assert O.shape == (B, H, S, D)
@@ -80,12 +107,12 @@ def _worker(rank, world, port, B, H, S, D, errq):
         raise
 
 
-@pytest.mark.parametrize("B,H", [(2, 4), (1, 6)])
-def test_gloo_world2_sharded_forward(B, H):
+@pytest.mark.parametrize("B,H,Hkv", [(2, 4, None), (1, 6, None), (2, 8, 2), (1, 8, 2)])
+def test_gloo_world2_sharded_forward(B, H, Hkv):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, B, H, 64, 32, errq)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, B, H, 64, 32, errq, Hkv)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
