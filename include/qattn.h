@@ -258,6 +258,16 @@ int qattn_jvp_fwd_x3_ex(const void* q_hi, const void* q_lo, const void* k_hi, co
                         void* out, void* tout, void* lse, long bh, long sq, long sk, int group,
                         int head_dim, float qks, float sm, void* stream);
 
+/* Primal-only forward of the JVP kernel (O, lse; no tangent operands or chains): the forward of
+ * AttentionJVP_autograd_function, whose jvp() then runs qattn_jvp_fwd_ex once.
+ * O / lse are bit-identical to those qattn_jvp_fwd_ex / qattn_jvp_fwd_x3_ex return for the same
+ * primals.  Arguments as those entries without the tangents. */
+int qattn_jvp_primal_ex(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
+                        long sq, long sk, int group, int head_dim, float qks, float sm, void* stream);
+int qattn_jvp_primal_x3_ex(const void* q_hi, const void* q_lo, const void* k_hi, const void* k_lo,
+                           const void* v_hi, const void* v_lo, void* out, void* lse, long bh, long sq,
+                           long sk, int group, int head_dim, float qks, float sm, void* stream);
+
 /* hi = bf16(x), lo = bf16(x - hi) (both round-to-nearest-even) for n fp32 elements, n % 4 == 0. */
 int qattn_split_bf16(const void* x, void* hi, void* lo, long n, void* stream);
 

@@ -13,7 +13,7 @@ Parity status
 The reference kernels cannot run here: every module imports ``helion`` (not installed, not
 installable offline), and stand-ins for absent libraries are not used.  This restatement is
 therefore pinned only by (a) the reference's own published test statistics (attention_jvp.py:
-305-317, attention_bf16.py:563), checked in ``tests/test_oracle_pins.py``, and (b) the reference's
+305-317, attention_bf16.py:563), checked in ``tests/test_oracle.py``, and (b) the reference's
 own fp32 oracle ``baseline_pytorch_attention`` (restated below).  Bit-level parity with the
 reference's kernels is **unpinned** (DESIGN.md §3).  The survey probe found
 this rounding contract bit-identical to the reference run eagerly; that probe is not re-run here.

@@ -61,6 +61,9 @@ SIGNATURES = {
     "qattn_jvp_fwd": [_vp] * 9 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
     "qattn_jvp_fwd_x3": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_jvp_fwd_ex": [_vp] * 9 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
+    "qattn_jvp_primal_ex": [_vp] * 5 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float, _vp],
+    "qattn_jvp_primal_x3_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float,
+                               _vp],
     "qattn_jvp_fwd_x3_ex": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _c_float,
                                          _vp],
     "qattn_split_bf16": [_vp, _vp, _vp, _c_long, _vp],

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from typing import Tuple
 
 import torch
@@ -131,7 +132,7 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
 # Largest dS workspace (bytes) the backward allocates to skip the dQ pass's recomputation of S,
 # dP, P and dS (qattn_int8_attn_bwd_ws); larger problems recompute (qattn_int8_attn_bwd_ex).  The
 # results are bit-identical either way.  1 B per score + 4 B per 32x32 tile: 2.2 GB at (4,32,4096).
-WS_MAX_BYTES = int(os.environ.get("QATTN_BWD_WS_MAX", 16 << 30))
+WS_MAX_BYTES = int(os.environ.get("QATTN_BWD_WS_MAX", 64 << 30))
 
 
 def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=None, causal=False,
@@ -244,25 +245,52 @@ def helion_atten_int8_hl_dot_bwd(
                           kv_heads=kv_heads)
 
 
+# bf16 images of q_i8 / k_i8 written by the forward's quantiser pass, handed from forward() to
+# setup_context() (a new-style forward has no ctx).  Keyed by id(q_i8); the entry is dropped with
+# q_i8, so a forward whose setup_context never runs (a direct Function.forward call) leaks nothing.
+_IMAGES: dict = {}
+
+
+def _stash_images(q_i8, q_bf, k_bf):
+    key = id(q_i8)
+    _IMAGES[key] = (weakref.ref(q_i8), q_bf, k_bf)
+    weakref.finalize(q_i8, _IMAGES.pop, key, None)
+
+
+def _take_images(q_i8):
+    e = _IMAGES.pop(id(q_i8), None)
+    if e is None or e[0]() is not q_i8:
+        return None, None
+    return e[1], e[2]
+
+
 class SageAttention3_Int8_autograd_function(Function):
-    """int8:20-95.  forward(q, k, v) -> 11-tuple
-    (O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv)."""
+    """int8:20-95, new-style like the reference: ``forward(q, k, v)`` (no ctx) + ``setup_context`` +
+    ``backward``.  forward returns the 11-tuple (O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, Bq,
+    Bkv); ``forward(q, k, v, causal)`` is an extension."""
 
     @staticmethod
-    def forward(ctx, q_fp16, k_fp16, v_fp16, *opts):
-        # opts: (causal,) -- an extension; the reference's apply(q, k, v) passes none
-        causal = bool(opts[0]) if opts else False
-        # The bf16 images of q_i8 / k_i8 the backward reads come out of the same quantiser pass
-        # when a gradient will be taken (kept on ctx, not returned: the 11-tuple is the reference's).
+    def forward(q_fp16, k_fp16, v_fp16, causal=False):
+        # The bf16 images of q_i8 / k_i8 the backward reads come out of the same quantiser pass when
+        # a gradient will be taken (handed to setup_context, not returned: the 11-tuple is the
+        # reference's).
         images = any(t.requires_grad for t in (q_fp16, k_fp16, v_fp16))
         O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean, q_bf, k_bf = _int8_forward(
-            q_fp16, k_fp16, v_fp16, smooth=True, images=images, causal=causal)
-        ctx.opts = (causal, k_fp16.shape[1], len(opts))
+            q_fp16, k_fp16, v_fp16, smooth=True, images=images, causal=bool(causal))
+        if images:
+            _stash_images(q_i8, q_bf, k_bf)
+        return O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, BQ, BKV
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        k_fp16 = inputs[1]
+        causal = bool(inputs[3]) if len(inputs) > 3 else False
+        O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, Bq, Bkv = output
         ctx.mark_non_differentiable(lse, k_mean, sq, sk, sv)  # int8:52-56
         ctx.save_for_backward(O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv)  # int8:58-64
-        ctx.images = (q_bf, k_bf)
-        ctx.args = (BQ, BKV)
-        return O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv, BQ, BKV
+        ctx.args = (Bq, Bkv)
+        ctx.images = _take_images(q_i8)
+        ctx.opts = (causal, k_fp16.shape[1], len(inputs) - 3)
 
     @staticmethod
     def backward(ctx, dO_fp16, _lse, _k_mean, _q_i8, _k_i8T, _v_i8, _sq, _sk, _sv, _Bq, _Bkv):
@@ -272,7 +300,7 @@ class SageAttention3_Int8_autograd_function(Function):
             raise _lib.QAttnError("qattn int8 backward is built for Bq = Bkv = 32")
         if dO_fp16 is None:
             dO_fp16 = torch.zeros_like(O)
-        q_bf, k_bf = ctx.images
+        q_bf, k_bf = ctx.images   # (None, None): the backward rebuilds them from q_i8 / k_i8
         ctx.images = None
         causal, kv_heads, nopts = ctx.opts
         dq, dk, dv = _int8_backward(dO_fp16, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf, k_bf,

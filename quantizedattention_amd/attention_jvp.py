@@ -35,20 +35,27 @@ def baseline_pytorch_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor
 def helion_attention_jvp_forward_fp32(q_fp32_input, k_fp32_input, v_fp32_input,
                                       tan_q_fp32_input, tan_k_fp32_input, tan_v_fp32_input):
     """jvp:33-195 -> (O fp32 [B,H,S,D], tO fp32 [B,H,S,D], lse fp32 [B*H, S])."""
+    return _jvp(q_fp32_input, k_fp32_input, v_fp32_input,
+                (tan_q_fp32_input, tan_k_fp32_input, tan_v_fp32_input))
+
+
+def _jvp(q_fp32_input, k_fp32_input, v_fp32_input, tangents):
+    """The kernel call.  ``tangents`` None runs the primal-only kernel (qattn_jvp_primal_ex: O and
+    lse, bit-identical to the tangent kernel's) and returns (O, None, lse)."""
     batch, head, q_tokens, q_head_dim = q_fp32_input.shape
     k_batch, k_head, k_tokens, k_head_dim = k_fp32_input.shape
     v_batch, v_head, v_tokens, v_head_dim = v_fp32_input.shape
     assert k_tokens == v_tokens, "input k_tokens must match v_tokens"  # jvp:78
     assert q_head_dim == k_fp32_input.size(-1) == v_fp32_input.size(-1), \
         "all head dimensions must match for q, k, v tensors"  # jvp:79
-    ins = (q_fp32_input, k_fp32_input, v_fp32_input, tan_q_fp32_input, tan_k_fp32_input,
-           tan_v_fp32_input)
+    prim = (q_fp32_input, k_fp32_input, v_fp32_input)
+    ins = prim + (tuple(tangents) if tangents is not None else ())
     _lib.require_gpu(*ins)
     if q_tokens % 32 or k_tokens % 32:
         raise _lib.QAttnError("qattn jvp: q and k tokens must be multiples of 32")
     if q_head_dim not in (64, 128):
         raise _lib.QAttnError("qattn jvp: head_dim must be 64 or 128")
-    for t, ref in zip(ins[3:], ins[:3]):
+    for t, ref in zip(ins[3:], prim):
         if t.shape != ref.shape:
             raise _lib.QAttnError("qattn jvp: tangents must have the primals' shapes")
     B, H, S, D = q_fp32_input.shape
@@ -59,18 +66,20 @@ def helion_attention_jvp_forward_fp32(q_fp32_input, k_fp32_input, v_fp32_input,
     group = H // Hkv
     dev = q_fp32_input.device
     O = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
-    tO = torch.empty_like(O)
+    tO = torch.empty_like(O) if tangents is not None else None
     lse = torch.empty((B * H, S), dtype=torch.float32, device=dev)
     qks = float(torch.tensor(1.0 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
     sm = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
     st = _lib.stream_of(q_fp32_input)
+    shape = (B * H, S, k_tokens, group, D, qks, sm, st)
     if all(t.dtype == torch.bfloat16 for t in ins):
         if k_tokens % 64:
             raise _lib.QAttnError("qattn jvp: k tokens must be a multiple of 64 for bf16 inputs")
-        q, k, v, tq, tk, tv = (t.contiguous() for t in ins)
-        _lib.call("qattn_jvp_fwd_ex", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(tq), _lib.ptr(tk),
-                  _lib.ptr(tv), _lib.ptr(O), _lib.ptr(tO), _lib.ptr(lse), B * H, S, k_tokens, group, D,
-                  qks, sm, st)
+        ptrs = [_lib.ptr(t.contiguous()) for t in ins]
+        if tangents is None:
+            _lib.call("qattn_jvp_primal_ex", *ptrs, _lib.ptr(O), _lib.ptr(lse), *shape)
+        else:
+            _lib.call("qattn_jvp_fwd_ex", *ptrs, _lib.ptr(O), _lib.ptr(tO), _lib.ptr(lse), *shape)
         return O, tO, lse
     imgs = []
     for t in ins:
@@ -79,8 +88,12 @@ def helion_attention_jvp_forward_fp32(q_fp32_input, k_fp32_input, v_fp32_input,
         lo = torch.empty_like(hi)
         _lib.call("qattn_split_bf16", _lib.ptr(x), _lib.ptr(hi), _lib.ptr(lo), x.numel(), st)
         imgs += [hi, lo]
-    _lib.call("qattn_jvp_fwd_x3_ex", *(_lib.ptr(t) for t in imgs), _lib.ptr(O), _lib.ptr(tO),
-              _lib.ptr(lse), B * H, S, k_tokens, group, D, qks, sm, st)
+    if tangents is None:
+        _lib.call("qattn_jvp_primal_x3_ex", *(_lib.ptr(t) for t in imgs), _lib.ptr(O), _lib.ptr(lse),
+                  *shape)
+    else:
+        _lib.call("qattn_jvp_fwd_x3_ex", *(_lib.ptr(t) for t in imgs), _lib.ptr(O), _lib.ptr(tO),
+                  _lib.ptr(lse), *shape)
     return O, tO, lse
 
 
@@ -95,17 +108,17 @@ class AttentionJVP_autograd_function(torch.autograd.Function):
     """Attention O = softmax(q k^T / sqrt(D)) v whose forward-mode derivative is the kernel's tO.
 
     ``torch.func.jvp(attention_jvp, (q, k, v), (tq, tk, tv))`` and ``torch.autograd.forward_ad``
-    dual tensors both dispatch to :meth:`jvp`.  The forward runs the same kernel with zero tangents
-    (so O matches the one the jvp call would produce); reverse mode is not provided, as in the
-    reference, which has no backward for this path.
+    dual tensors both dispatch to :meth:`jvp`.  The forward runs the primal-only kernel
+    (qattn_jvp_primal_ex: no tangent chains, O bit-identical to the tangent kernel's), so a
+    ``torch.func.jvp`` call costs one primal and one tangent launch; reverse mode is not provided,
+    as in the reference, which has no backward for this path.
     """
 
     @staticmethod
     def forward(q, k, v):
         q, k, v = _plain(q), _plain(k), _plain(v)
         with torch._C._DisableFuncTorch():
-            O, _tO, _lse = helion_attention_jvp_forward_fp32(q, k, v, torch.zeros_like(q),
-                                                             torch.zeros_like(k), torch.zeros_like(v))
+            O, _tO, _lse = _jvp(q, k, v, None)
         return O
 
     @staticmethod

@@ -354,7 +354,8 @@ QA_DEVICE void ring_wait_barrier() {
 // + soffset (wave-uniform tile offset, SGPR); LDS destination = M0 + 16*lane (4*lane for dword).
 // Per piece only the M0 write and the load issue: no 64-bit per-lane address arithmetic.  M0 is
 // written without save/restore: the kernels that use these helpers contain no other M0 use
-// (tests/test_isa.py checks the disassembly of every kernel that uses them), and the M0 -> LDS-DMA hazard takes one s_nop.
+// (tests/test_isa.py proves on the emitted code that hipcc itself never reads or writes M0 and that every
+// LDS-DMA follows an M0 write in its own asm block), and the M0 -> LDS-DMA hazard takes one s_nop.
 QA_DEVICE v4u make_rsrc(const void* base, unsigned bytes) {
   const unsigned long a = (unsigned long)base;
   v4u r;

@@ -21,14 +21,20 @@ namespace qattn {
 // hi*hi + hi*lo + lo*hi + lo*lo, exact up to the split residual |x - hi - lo| <= 2^-17 |x|.
 // 4x the MFMAs of the bf16 mode.  Measured vs torch.func.jvp in float64 (tools/jvp_err.py): O within
 // 6e-6, tO within 8e-6 at max|tO| = 1.35 (dropping lo*lo: tO 2.7e-5).
-template <int D, bool X3>
+// TAN = false is the primal-only kernel (O and lse, no tangent chains or tangent operands): the
+// forward of AttentionJVP_autograd_function.  Its S, P, l and O arithmetic is the
+// same instruction sequence as the tangent kernel's, so O / lse are bit-identical to the ones
+// qattn_jvp_fwd returns (tests/test_gpu_jvp.py).
+template <int D, bool X3, bool TAN = true>
 struct JvpCfg {
   static constexpr int KB = X3 ? 32 : 64;     // keys per stage
   static constexpr int NIMG = X3 ? 2 : 1;     // bf16 images per operand
   static constexpr int ROWB = 2 * D;
   static constexpr int NCH = ROWB / 16;
   static constexpr int TILE = KB * ROWB;
-  static constexpr int STAGE = 4 * NIMG * TILE;  // K, tK, V, tV (x hi/lo)
+  static constexpr int NOPS = TAN ? 4 : 2;    // K, tK, V, tV / K, V
+  static constexpr int STAGE = NOPS * NIMG * TILE;
+  static constexpr int SK = 0, STK = 1, SV = TAN ? 2 : 1, STV = 3;   // operand slots in a stage
   static constexpr int NKS = D / 16;
   static constexpr int NDB = D / 32;
 };
@@ -80,9 +86,9 @@ struct JvpArgs {
   float qks, sm;
 };
 
-template <int D, bool X3>
+template <int D, bool X3, bool TAN>
 __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
-  using C = JvpCfg<D, X3>;
+  using C = JvpCfg<D, X3, TAN>;
   constexpr int NI = C::NIMG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int Sq = a.Sq, Sk = a.Sk;
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
 #pragma unroll
       for (int s = 0; s < C::NKS; ++s) {
         qf[x][s] = *reinterpret_cast<const v8bf*>(a.q[x] + r * D + 16 * s + 8 * h);
-        tqf[x][s] = *reinterpret_cast<const v8bf*>(a.tq[x] + r * D + 16 * s + 8 * h);
+        if constexpr (TAN) tqf[x][s] = *reinterpret_cast<const v8bf*>(a.tq[x] + r * D + 16 * s + 8 * h);
       }
   }
   v16f o[C::NDB], ab[C::NDB];
@@ -112,16 +118,18 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
 
   const long kv0 = (long)(bh / a.G) * Sk * D;
   const int nkb = Sk / C::KB;
-  // stage layout: [K x NI][tK x NI][V x NI][tV x NI]
+  // stage layout: [K x NI][tK x NI][V x NI][tV x NI]  (primal-only: [K x NI][V x NI])
   auto stage = [&](int kb, int buf) {
     char* base = smem + buf * C::STAGE;
     const long off = (long)kb * C::TILE;
 #pragma unroll
     for (int x = 0; x < NI; ++x) {
-      dma_tile<D, X3, false>(reinterpret_cast<const char*>(a.k[x] + kv0) + off, base + (0 * NI + x) * C::TILE, wave, lane);
-      dma_tile<D, X3, false>(reinterpret_cast<const char*>(a.tk[x] + kv0) + off, base + (1 * NI + x) * C::TILE, wave, lane);
-      dma_tile<D, X3, true>(reinterpret_cast<const char*>(a.v[x] + kv0) + off, base + (2 * NI + x) * C::TILE, wave, lane);
-      dma_tile<D, X3, true>(reinterpret_cast<const char*>(a.tv[x] + kv0) + off, base + (3 * NI + x) * C::TILE, wave, lane);
+      dma_tile<D, X3, false>(reinterpret_cast<const char*>(a.k[x] + kv0) + off, base + (C::SK * NI + x) * C::TILE, wave, lane);
+      dma_tile<D, X3, true>(reinterpret_cast<const char*>(a.v[x] + kv0) + off, base + (C::SV * NI + x) * C::TILE, wave, lane);
+      if constexpr (TAN) {
+        dma_tile<D, X3, false>(reinterpret_cast<const char*>(a.tk[x] + kv0) + off, base + (C::STK * NI + x) * C::TILE, wave, lane);
+        dma_tile<D, X3, true>(reinterpret_cast<const char*>(a.tv[x] + kv0) + off, base + (C::STV * NI + x) * C::TILE, wave, lane);
+      }
     }
   };
   // hi*hi (+ hi*lo + lo*hi + lo*lo in X3): acc += A.B for split operands
@@ -151,14 +159,16 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
           v8bf ka[NI], tka[NI], qq[NI], tqq[NI];
 #pragma unroll
           for (int x = 0; x < NI; ++x) {
-            ka[x] = *reinterpret_cast<const v8bf*>(base + (0 * NI + x) * C::TILE + off);
-            tka[x] = *reinterpret_cast<const v8bf*>(base + (1 * NI + x) * C::TILE + off);
+            ka[x] = *reinterpret_cast<const v8bf*>(base + (C::SK * NI + x) * C::TILE + off);
+            if constexpr (TAN) tka[x] = *reinterpret_cast<const v8bf*>(base + (C::STK * NI + x) * C::TILE + off);
             qq[x] = qf[x][s];
-            tqq[x] = tqf[x][s];
+            if constexpr (TAN) tqq[x] = tqf[x][s];
           }
           sacc = mm(ka, qq, sacc);        // S^T = K q^T
-          tacc = mm(ka, tqq, tacc);       // tS^T = K tq^T + tK q^T   (jvp:148-153)
-          tacc = mm(tka, qq, tacc);
+          if constexpr (TAN) {
+            tacc = mm(ka, tqq, tacc);     // tS^T = K tq^T + tK q^T   (jvp:148-153)
+            tacc = mm(tka, qq, tacc);
+          }
         }
         float rl = -INFINITY;
 #pragma unroll
@@ -169,19 +179,24 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           p[i] = exp2_f32(sacc[i] * qks - nm);     // jvp:160-161
-          hh[i] = p[i] * (tacc[i] * sm);           // jvp:152-153,176
           lt += p[i];
-          rt += hh[i];
+          if constexpr (TAN) {
+            hh[i] = p[i] * (tacc[i] * sm);         // jvp:152-153,176
+            rt += hh[i];
+          }
         }
         lt += xor32_f(lt);
-        rt += xor32_f(rt);
+        if constexpr (TAN) rt += xor32_f(rt);
         const float rs = exp2_f32(m - nm);         // jvp:164
         l = l * rs + lt;
-        racc = racc * rs + rt;                     // jvp:178
+        if constexpr (TAN) racc = racc * rs + rt;  // jvp:178
         m = nm;
         if (__ballot(rs != 1.0f)) {
 #pragma unroll
-          for (int b = 0; b < C::NDB; ++b) { o[b] *= rs; ab[b] *= rs; }
+          for (int b = 0; b < C::NDB; ++b) {
+            o[b] *= rs;
+            if constexpr (TAN) ab[b] *= rs;
+          }
         }
         v8bf pb[2][NI], hb[2][NI];
 #pragma unroll
@@ -192,10 +207,11 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
             const float p0 = p[8 * s + 2 * j], p1 = p[8 * s + 2 * j + 1];
             const float h0 = hh[8 * s + 2 * j], h1 = hh[8 * s + 2 * j + 1];
             pp[0][j] = pk_bf16(p0, p1);
-            hp[0][j] = pk_bf16(h0, h1);
+            if constexpr (TAN) hp[0][j] = pk_bf16(h0, h1);
             if constexpr (X3) {
               pp[1][j] = pk_bf16(p0 - __uint_as_float(pp[0][j] << 16), p1 - __uint_as_float(pp[0][j] & 0xffff0000u));
-              hp[1][j] = pk_bf16(h0 - __uint_as_float(hp[0][j] << 16), h1 - __uint_as_float(hp[0][j] & 0xffff0000u));
+              if constexpr (TAN)
+                hp[1][j] = pk_bf16(h0 - __uint_as_float(hp[0][j] << 16), h1 - __uint_as_float(hp[0][j] & 0xffff0000u));
             }
           }
 #pragma unroll
@@ -211,12 +227,14 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
             v8bf va[NI], tva[NI];
 #pragma unroll
             for (int x = 0; x < NI; ++x) {
-              va[x] = jtr_frag<D>(base + (2 * NI + x) * C::TILE, 32 * u + 16 * s, b, lane);
-              tva[x] = jtr_frag<D>(base + (3 * NI + x) * C::TILE, 32 * u + 16 * s, b, lane);
+              va[x] = jtr_frag<D>(base + (C::SV * NI + x) * C::TILE, 32 * u + 16 * s, b, lane);
+              if constexpr (TAN) tva[x] = jtr_frag<D>(base + (C::STV * NI + x) * C::TILE, 32 * u + 16 * s, b, lane);
             }
             o[b] = mm(va, pb[s], o[b]);      // jvp:171
-            ab[b] = mm(tva, pb[s], ab[b]);   // jvp:173-174
-            ab[b] = mm(va, hb[s], ab[b]);    // jvp:180-181
+            if constexpr (TAN) {
+              ab[b] = mm(tva, pb[s], ab[b]); // jvp:173-174
+              ab[b] = mm(va, hb[s], ab[b]);  // jvp:180-181
+            }
           }
         }
       }
@@ -235,10 +253,10 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
       for (int j = 0; j < 4; ++j) {
         const float of = o[b][4 * g + j] / l;                   // jvp:188
         wo[j] = of;
-        wt[j] = (ab[b][4 * g + j] - racc * of) / l;             // jvp:190
+        if constexpr (TAN) wt[j] = (ab[b][4 * g + j] - racc * of) / l;   // jvp:190
       }
       *reinterpret_cast<v4f*>(a.out + r * D + 32 * b + 8 * g + 4 * h) = wo;
-      *reinterpret_cast<v4f*>(a.tout + r * D + 32 * b + 8 * g + 4 * h) = wt;
+      if constexpr (TAN) *reinterpret_cast<v4f*>(a.tout + r * D + 32 * b + 8 * g + 4 * h) = wt;
     }
   }
 }
@@ -260,12 +278,13 @@ __global__ void split_bf16_kernel(const float* __restrict__ x, __bf16* __restric
 
 using namespace qattn;
 
-template <int D, bool X3>
+template <int D, bool X3, bool TAN = true>
 static int launch_jvp(const JvpArgs& a, long bh, long sq, hipStream_t st) {
-  constexpr int lds = 2 * JvpCfg<D, X3>::STAGE;
-  hipFuncSetAttribute((const void*)jvp_fwd_kernel<D, X3>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  constexpr int lds = 2 * JvpCfg<D, X3, TAN>::STAGE;
+  (void)hipFuncSetAttribute((const void*)jvp_fwd_kernel<D, X3, TAN>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   const int nq = (int)((sq + 127) / 128);
-  hipLaunchKernelGGL((jvp_fwd_kernel<D, X3>), dim3((unsigned)(nq * bh)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((jvp_fwd_kernel<D, X3, TAN>), dim3((unsigned)(nq * bh)), dim3(256), lds, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -333,6 +352,37 @@ extern "C" int qattn_jvp_fwd_x3(const void* q_hi, const void* q_lo, const void* 
                                 float qks, float sm, void* stream) {
   return qattn_jvp_fwd_x3_ex(q_hi, q_lo, k_hi, k_lo, v_hi, v_lo, tq_hi, tq_lo, tk_hi, tk_lo, tv_hi, tv_lo,
                              out, tout, lse, bh, sq, sk, 1, head_dim, qks, sm, stream);
+}
+
+// Primal-only launches (O, lse; no tangents): bit-identical O / lse to qattn_jvp_fwd_ex /
+// qattn_jvp_fwd_x3_ex on the same primals.
+extern "C" int qattn_jvp_primal_ex(const void* q, const void* k, const void* v, void* out, void* lse,
+                                   long bh, long sq, long sk, int group, int head_dim, float qks,
+                                   float sm, void* stream) {
+  if (sq % 32 != 0 || sk % 64 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128))
+    return 1;
+  if (bh == 0 || sq == 0) return 0;
+  const void* img[6] = {q, k, v, q, k, v};
+  const JvpArgs a = jvp_args(img, out, out, lse, bh, sq, sk, group, qks, sm, 1);
+  hipStream_t st = (hipStream_t)stream;
+  return head_dim == 128 ? launch_jvp<128, false, false>(a, bh, sq, st)
+                         : launch_jvp<64, false, false>(a, bh, sq, st);
+}
+
+extern "C" int qattn_jvp_primal_x3_ex(const void* q_hi, const void* q_lo, const void* k_hi,
+                                      const void* k_lo, const void* v_hi, const void* v_lo, void* out,
+                                      void* lse, long bh, long sq, long sk, int group, int head_dim,
+                                      float qks, float sm, void* stream) {
+  if (sq % 32 != 0 || sk % 32 != 0 || group < 1 || bh % group != 0 ||
+      (head_dim != 64 && head_dim != 128))
+    return 1;
+  if (bh == 0 || sq == 0) return 0;
+  const void* img[12] = {q_hi, q_lo, k_hi, k_lo, v_hi, v_lo, q_hi, q_lo, k_hi, k_lo, v_hi, v_lo};
+  const JvpArgs a = jvp_args(img, out, out, lse, bh, sq, sk, group, qks, sm, 2);
+  hipStream_t st = (hipStream_t)stream;
+  return head_dim == 128 ? launch_jvp<128, true, false>(a, bh, sq, st)
+                         : launch_jvp<64, true, false>(a, bh, sq, st);
 }
 
 extern "C" int qattn_split_bf16(const void* x, void* hi, void* lo, long n, void* stream) {

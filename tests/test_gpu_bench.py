@@ -25,8 +25,10 @@ def test_bench_json_contract():
         assert key in d, key
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and "workload" in d["config"]
+    assert "(1,4,1024,128)" in d["config"]["workload"]
     rf = d["roofline"]
     assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s")
     assert 0 < rf["frac"] < 1 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] in ("port", "reference") and cb["cores"] >= 1
+    assert cb["logical_cpus"] >= cb["cores"] and "cpu_model" in cb

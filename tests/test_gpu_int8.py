@@ -171,3 +171,29 @@ def test_quant_image_and_bwd_prep(lib):
     Dref = (x.cpu().float() * O.cpu().float()).half().float().sum(-1).half().float()
     assert torch.equal(LD[:, 0].cpu(), lse.cpu().float())
     assert (LD[:, 1].cpu() - Dref).abs().max().item() <= 2 * 2.0 ** -10 * Dref.abs().max().item()
+
+
+def test_sage_function_new_style(lib):
+    """The autograd Function is new-style like the reference (int8:20-65): a direct
+    Function.forward(q, k, v) returns the 11-tuple, and torch.func.grad runs through it with the same
+    gradients as .backward() (which takes the bf16 images from the forward's quantiser pass; the
+    functorch path may rebuild them from q_i8 / k_i8 — bit-identical either way)."""
+    from quantizedattention_amd.attention_int8 import (SageAttention3_Int8_autograd_function as F,
+                                                       sage_attention_3_int8)
+    shape = (1, 2, 128, 128)
+    q, k, v = [t.half().cuda() for t in _inputs(shape, seed=51)]
+    outs = F.forward(q, k, v)
+    assert len(outs) == 11 and outs[9] == 32 and outs[10] == 32
+    assert outs[4].shape == (128, 2 * 128) and outs[4].stride() == (1, 128)
+    ref = sage_attention_3_int8(q, k, v)
+    assert torch.equal(outs[0], ref)
+    w = torch.randn(shape, generator=torch.Generator().manual_seed(52)).cuda()
+
+    def loss(q_, k_, v_):
+        return (sage_attention_3_int8(q_, k_, v_).float() * w).sum()
+    gq, gk, gv = torch.func.grad(loss, argnums=(0, 1, 2))(q, k, v)
+    qd, kd, vd = (t.clone().requires_grad_(True) for t in (q, k, v))
+    loss(qd, kd, vd).backward()
+    assert torch.equal(gq, qd.grad) and torch.equal(gk, kd.grad) and torch.equal(gv, vd.grad)
+    from quantizedattention_amd import attention_int8
+    assert not attention_int8._IMAGES, "image hand-off entries leaked"

@@ -114,3 +114,20 @@ def test_jvp_grouped_query(lib, dtype, shape):
     assert (O.cpu().double() - Or).abs().max().item() <= tol
     scale = max(1.0, tOr.abs().max().item())
     assert (tO.cpu().double() - tOr).abs().max().item() <= tol * scale
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(2, 4, 2, 256, 192, 128), (1, 2, 2, 96, 128, 64)])
+def test_jvp_primal_only_bit_identical(lib, dtype, shape):
+    """The primal-only kernel (the N1 Function's forward) returns the tangent kernel's O and lse
+    bit for bit: one primal + one tangent launch per torch.func.jvp call."""
+    from quantizedattention_amd.attention_jvp import _jvp
+    B, H, Hkv, Sq, Sk, D = shape
+    g = torch.Generator().manual_seed(13)
+    q, tq = (torch.randn((B, H, Sq, D), generator=g).to(dtype).cuda() for _ in range(2))
+    k, v, tk, tv = (torch.randn((B, Hkv, Sk, D), generator=g).to(dtype).cuda() for _ in range(4))
+    O, tO, lse = _jvp(q, k, v, (tq, tk, tv))
+    Op, none, lsep = _jvp(q, k, v, None)
+    torch.cuda.synchronize()
+    assert none is None
+    assert torch.equal(O, Op) and torch.equal(lse, lsep)

@@ -1,0 +1,104 @@
+"""Disassembly check of the M0 contract of the LDS-DMA helpers (CPU: hipcc cross-compiles gfx950).
+
+The buffer / global LDS-DMA helpers in csrc/common.h (``dma16_buf``, ``dma4_buf``, ``glds*``) write
+M0 from inline asm and issue the DMA in the same asm block.  M0 is a reserved register to hipcc, so
+it cannot be listed as a clobber; instead this test proves, on the code hipcc actually emits for
+every product kernel, that the compiler never touches M0 itself:
+
+  * every instruction that names ``m0`` lies inside an inline-asm block (``;;#ASMSTART`` ..
+    ``;;#ASMEND``);
+  * every LDS-DMA instruction (``buffer_load_* ... lds``, ``global_load_lds_*``) lies inside an asm
+    block that wrote M0 before it;
+  * no instruction that reads M0 implicitly (movrel, sendmsg, GWS / append / consume, interp) is
+    emitted anywhere.
+
+If a future compiler keeps a live value in M0 across these asm blocks, or emits its own LDS-DMA or
+M0 user, this test fails instead of the DMA destinations silently moving.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "quantizedattention_amd" / "csrc"
+HIPCC = "/opt/rocm/bin/hipcc"
+
+M0_IMPLICIT = re.compile(r"^\s*(s_movrel|v_movrel|s_sendmsg|ds_gws|ds_append|ds_consume|v_interp|"
+                         r"s_ttracedata|v_writelane_b32_e64\s+\S+,\s*m0)")
+DMA = re.compile(r"^\s*(buffer_load_\w+\s.*\blds\b|global_load_lds_\w+)")
+M0_WRITE = re.compile(r"^\s*s_mov_b32\s+m0\s*,")
+
+
+def _device_asm(src: Path, out_dir: Path) -> str:
+    from quantizedattention_amd.build import CFLAGS, FILE_FLAGS
+    flags = [f for f in CFLAGS if f not in ("-fPIC",)]
+    out = out_dir / (src.stem + ".s")
+    cmd = [HIPCC, *flags, *FILE_FLAGS.get(src.name, []), "--cuda-device-only", "-S", str(src),
+           "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc -S failed for {src.name}:\n{r.stderr[-2000:]}")
+    return out.read_text()
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    if not Path(HIPCC).exists():
+        pytest.skip("hipcc not available")
+    d = tmp_path_factory.mktemp("isa")
+    srcs = sorted(CSRC.glob("*.hip"))
+    with cf.ThreadPoolExecutor(max_workers=4) as ex:
+        texts = list(ex.map(lambda s: _device_asm(s, d), srcs))
+    return dict(zip((s.name for s in srcs), texts))
+
+
+def _check(text: str) -> tuple[int, list[str]]:
+    """Returns (number of LDS-DMA instructions seen, violations)."""
+    bad, n_dma = [], 0
+    in_asm, m0_set = False, False
+    for no, line in enumerate(text.split("\n"), 1):
+        t = line.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm, m0_set = True, False
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if not t or t.startswith((";", ".")):
+            continue
+        code = t.split(";")[0]
+        if M0_IMPLICIT.match(code):
+            bad.append(f"line {no}: implicit M0 user {code!r}")
+        if DMA.match(code):
+            n_dma += 1
+            if not (in_asm and m0_set):
+                bad.append(f"line {no}: LDS-DMA without an M0 write in its own asm block: {code!r}")
+        if re.search(r"\bm0\b", code):
+            if not in_asm:
+                bad.append(f"line {no}: compiler-emitted M0 access {code!r}")
+            elif M0_WRITE.match(code):
+                m0_set = True
+    return n_dma, bad
+
+
+def test_every_kernel_source_keeps_the_m0_contract(asm):
+    total = 0
+    for name, text in asm.items():
+        n, bad = _check(text)
+        total += n
+        assert not bad, f"{name}: " + "; ".join(bad[:5])
+    assert total > 0, "no LDS-DMA found: the pattern no longer matches the emitted code"
+
+
+def test_checker_flags_a_compiler_m0_use():
+    ok = ";;#ASMSTART\n\ts_mov_b32 m0, s4\n\ts_nop 0\n\tbuffer_load_dwordx4 v1, s[0:3], s5 offen lds\n;;#ASMEND\n"
+    assert _check(ok) == (1, [])
+    n, bad = _check(ok + "\ts_mov_b32 m0, -1\n\tds_read_b32 v0, v1\n")
+    assert bad and "compiler-emitted" in bad[0]
+    n, bad = _check(";;#ASMSTART\n\tbuffer_load_dword v1, s[0:3], s5 offen lds\n;;#ASMEND\n")
+    assert bad and "without an M0 write" in bad[0]

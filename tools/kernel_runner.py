@@ -1,6 +1,6 @@
 """Launch one kernel of the int8 / bf16 paths N times at the headline shape (for rocprofv3 passes).
 
-    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd, int8_fwd_i8, int8_dkdv, int8_dv, int8_dk, int8_dq, int8_all, bf16_fwd,
+    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd (f16 P.V), int8_fwd_i8 (default), int8_dkdv, int8_dv, int8_dk, int8_dq, int8_all, bf16_fwd,
                                                            bf16_bwd, jvp, quant
 """
 import math
@@ -17,7 +17,7 @@ from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp
 
 name = sys.argv[1]
 if name == "int8_all":  # every int8 attention kernel once per rep, in step order
-    names = ["int8_fwd", "int8_dkdv_ws", "int8_dqw", "int8_dkdv", "int8_dq"]
+    names = ["int8_fwd_i8", "int8_fwd", "int8_dkdv_ws", "int8_dqw", "int8_dkdv", "int8_dq"]
 else:
     names = [name]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5

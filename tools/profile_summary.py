@@ -23,7 +23,8 @@ PROF = os.path.join(ROOT, "profiles")
 
 # bench.py kernel keys -> normalised rocprof kernel-name patterns (D = 128 instantiations)
 KEYS = {
-    "int8_attn_fwd_kernel": r"int8_attn_fwd_kernel(<128(,0)?>|ILi128ELi0E|ILi128EE)",
+    "int8_attn_fwd_kernel": r"int8_attn_fwd_kernel(<128, ?1, ?false>|ILi128ELi1ELb0E)",
+    "int8_attn_fwd_kernel<f16 P.V>": r"int8_attn_fwd_kernel(<128, ?0, ?false>|ILi128ELi0ELb0E)",
     "int8_bwd_dkdv_kernel<dK+dV>": r"int8_bwd_kernel(<128, ?3, ?false, ?false>|ILi128ELi3ELb0ELb0E)",
     "int8_bwd_dq_kernel": r"int8_bwd_kernel(<128, ?2|ILi128ELi2E)",
     "int8_bwd_dkdv_kernel<dK+dV, dS out>": r"int8_bwd_kernel(<128, ?3, ?false, ?true>|ILi128ELi3ELb0ELb1E)",
@@ -108,8 +109,12 @@ def main():
         json.dump({"note": "FETCH_SIZE/WRITE_SIZE are KB per dispatch from rocprofv3; FETCH doubled "
                            "per MI355X_MICROARCH.md (gfx950 reports half of wide streaming reads)",
                    "kernels": out}, f, indent=1)
+    sys.path.insert(0, ROOT)
+    from bench import source_hash
     with open(os.path.join(PROF, "traffic_latest.json"), "w") as f:
-        json.dump(traffic, f, indent=1)
+        # bench.py reports these only while the kernel sources hash to source_sha256
+        json.dump({"tag": tag, "source_sha256": source_hash(), "shape": [4, 32, 4096, 128],
+                   "traffic": traffic}, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
