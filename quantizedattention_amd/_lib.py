@@ -168,6 +168,18 @@ def call(name: str, *args) -> None:
         raise QAttnError(f"{name}: kernel launch failed (status {rc})")
 
 
+def plain(t):
+    """The tensor under any functorch wrappers (torch.func.grad / vjp / jvp hand custom Functions'
+    backward and jvp rules GradTrackingTensors, which have no storage).  Kernel launches run on the
+    plain tensors inside ``torch._C._DisableFuncTorch()``; torch wraps the plain results again."""
+    if not isinstance(t, torch.Tensor):
+        return t
+    from torch._C._functorch import get_unwrapped, is_functorch_wrapped_tensor
+    while is_functorch_wrapped_tensor(t):
+        t = get_unwrapped(t)
+    return t
+
+
 def require_gpu(*tensors: torch.Tensor) -> None:
     for t in tensors:
         if not t.is_cuda:

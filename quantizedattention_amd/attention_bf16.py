@@ -158,12 +158,13 @@ class FlashAttention_2_BF16_autograd_function(Function):
 
     @staticmethod
     def backward(ctx, dO, _lse):
-        q_fp16, k_fp16, v_bf16, O_fp32, lse_fp32 = ctx.saved_tensors
+        # plain tensors under torch.func transforms (_lib.plain); a no-op otherwise
+        q_fp16, k_fp16, v_bf16, O_fp32, lse_fp32 = (_lib.plain(t) for t in ctx.saved_tensors)
         causal = ctx.args
-        if dO is None:
-            dO = torch.zeros_like(O_fp32)
-        dq, dk, dv = helion_flash_atten_2_algo_4_bwd(q_fp16, k_fp16, v_bf16, O_fp32, lse_fp32,
-                                                     causal, dO)
+        with torch._C._DisableFuncTorch():
+            dO = torch.zeros_like(O_fp32) if dO is None else _lib.plain(dO)
+            dq, dk, dv = helion_flash_atten_2_algo_4_bwd(q_fp16, k_fp16, v_bf16, O_fp32, lse_fp32,
+                                                         causal, dO)
         return dq, dk, dv, None  # bf16:85
 
 

@@ -294,17 +294,18 @@ class SageAttention3_Int8_autograd_function(Function):
 
     @staticmethod
     def backward(ctx, dO_fp16, _lse, _k_mean, _q_i8, _k_i8T, _v_i8, _sq, _sk, _sv, _Bq, _Bkv):
-        O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv = ctx.saved_tensors
+        # plain tensors under torch.func transforms (_lib.plain); a no-op otherwise
+        O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv = (_lib.plain(t) for t in ctx.saved_tensors)
         Bq, Bkv = ctx.args
         if Bq != BQ or Bkv != BKV:
             raise _lib.QAttnError("qattn int8 backward is built for Bq = Bkv = 32")
-        if dO_fp16 is None:
-            dO_fp16 = torch.zeros_like(O)
         q_bf, k_bf = ctx.images   # (None, None): the backward rebuilds them from q_i8 / k_i8
         ctx.images = None
         causal, kv_heads, nopts = ctx.opts
-        dq, dk, dv = _int8_backward(dO_fp16, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf, k_bf,
-                                    causal=causal, kv_heads=kv_heads)
+        with torch._C._DisableFuncTorch():
+            dO_fp16 = torch.zeros_like(O) if dO_fp16 is None else _lib.plain(dO_fp16)
+            dq, dk, dv = _int8_backward(dO_fp16, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf, k_bf,
+                                        causal=causal, kv_heads=kv_heads)
         return (dq, dk, dv) + (None,) * nopts
 
 

