@@ -168,6 +168,8 @@ struct SmTile {
   v2h d[8];       // f16(S - rm) for the 16 scores of this lane
   float er;       // exp2(rm - m)
   float cpv;      // PV_F16: sp = f16(er / 127) (as f32); PV_I8: the tile's dequantisation er/127*sv
+  v2h pi[8];      // CAUSAL diagonal tiles: P_i8 by the reference's literal chain (f16 integers)
+  bool diag;      // (wave-uniform) this tile crosses the wave's causal diagonal
 };
 
 // Shapes: BH = batch * query heads, Sq query and Sk key tokens per head; query head
@@ -262,6 +264,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) o[b] = v16f{};
   _Float16 m = (_Float16)(-INFINITY);
+  _Float16 mt = (_Float16)(-INFINITY);   // CAUSAL: the reference's (undeferred) running max
   float l = 0.f;      // per-lane partial (this lane's key half); the reference's l = 1 is wiped by r = 0
   float obias = 0.f;  // PV_I8: sum of the tile dequantisation factors (the KMAG bias of O is KMAG * obias)
 
@@ -323,6 +326,28 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     const v2h rm2 = {rm, rm};
 #pragma unroll
     for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;   // f16(S - rm)  (int8:211, 232-236)
+    if constexpr (CAUSAL) {
+      // Diagonal tiles keep few keys per row, where one P_i8 step weighs much in O: there P_i8
+      // follows the reference chain literally (int8:205-237): next_m = max(m, rm) with the
+      // undeferred running max, P = exp2(f32(f16(S - next_m))), sp = exp2(f32(f16(rm - next_m)))/127
+      // and P_i8 = trunc(P / sp), IEEE fp32 divisions.  Other tiles use 127 exp2(f16(S - rm)) (the
+      // same value up to the last bits, which only matter when few keys share the row sum).
+      const bool kept = mx != INT_MIN;     // the row keeps a key of this tile
+      const _Float16 nm_ref = (kept && rm > mt) ? rm : mt;
+      if (kept) mt = nm_ref;
+      st.diag = diag;
+      if (diag) {
+        const float spr = exp2_f32((float)(_Float16)((float)rm - (float)nm_ref)) / 127.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float dr = (float)(_Float16)((float)s2[j][e] - (float)nm_ref);
+            const float pr = __builtin_truncf(exp2_f32(dr) / spr);
+            st.pi[j][e] = (acc[2 * j + e] == INT_MIN || !kept) ? (_Float16)0.0f : (_Float16)pr;
+          }
+      }
+    }
     if (diag) {
       const _Float16 ninf = (_Float16)(-INFINITY);
 #pragma unroll
@@ -358,6 +383,21 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     // row sum of e: packed f16 adds (pairs, then sums of 4 and 8 values <= 8), one f32 mix-add
     const v2h s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
     l = fmaf(pk_hsum(s), st.er, l);
+    if (CAUSAL && st.diag) {   // the literal-chain P_i8 of a diagonal tile (sm1)
+      if constexpr (PV == PV_F16) {
+        const _Float16 sp = (_Float16)st.cpv;
+        const v2h sp2 = {sp, sp};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pw[j / 4][j % 4] = __builtin_bit_cast(unsigned, st.pi[j] * sp2);
+      } else {
+        const v2h k1024 = {(_Float16)1024.0f, (_Float16)1024.0f};
+        unsigned y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = __builtin_bit_cast(unsigned, st.pi[j] + k1024);
+        pw[0] = __builtin_bit_cast(v4u, pack_p_index(y));
+      }
+      return;
+    }
     if constexpr (PV == PV_F16) {
       const _Float16 sp = (_Float16)st.cpv;
       const v2h sp2 = {sp, sp};

@@ -2,9 +2,10 @@
 counterpart): grouped-query attention (Hq a multiple of Hkv), Sq != Sk and causal masking, against
 the oracle's restatement of the same extension (oracle/restate.py int8_fwd / int8_bwd).
 
-Tolerances as tests/test_gpu_int8.py: quantisation bit-exact; O max-abs <= 1e-2 (causal: 5e-2 on
-the first 32 rows, which keep fewer than 32 keys); lse <= 2 fp16 ulp (+1e-3); grads relL2 <= 0.05
-vs the oracle.  Parity with the reference is not defined here (the
+Tolerances as tests/test_gpu_int8.py: quantisation bit-exact; O max-abs <= 1e-2 on every row
+(causal rows that keep only a few keys included: on the tiles crossing the diagonal the kernel's P_i8
+follows the reference chain literally); lse <= 2 fp16 ulp (+1e-3); grads relL2 <= 0.05 vs the
+oracle.  Parity with the reference is not defined here (the
 reference has no such shapes): the oracle pins the documented semantics.
 """
 import pytest
@@ -39,7 +40,7 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("shape", SHAPES + [(1, 8, 8, 256, 256, 128), (1, 4, 2, 96, 224, 64)])
 @pytest.mark.parametrize("causal", [False, True])
 def test_int8_fwd_gqa_causal(lib, shape, causal, pv):
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
@@ -51,12 +52,6 @@ def test_int8_fwd_gqa_causal(lib, shape, causal, pv):
         assert out[i].shape == ref[i].shape and torch.equal(out[i].cpu(), ref[i]), i
     assert out[0].shape == ref[0].shape
     diff = (out[0].float().cpu() - ref[0].float()).abs()
-    if causal:
-        # rows that keep fewer than 32 keys: one P_i8 = trunc(127 e) step -- where the kernel's f16
-        # exponential and the oracle's fp32 one straddle an integer -- moves O by |v|/127 divided by
-        # a row sum of only a few terms, so these rows get 5e-2; every other row the 1e-2 bar
-        assert diff[:, :, :32].max().item() <= 5e-2, diff[:, :, :32].max().item()
-        diff = diff[:, :, 32:]
     err = diff.max().item()
     assert err <= 1e-2, err
     lerr = (out[1].float().cpu() - ref[1].float()).abs()
@@ -110,7 +105,7 @@ def test_int8_autograd_gqa_causal(lib):
     ks, km = R.k_smooth(k)
     ref = R.int8_fwd(q, ks, v, causal=True)
     diff = (O.detach().float().cpu() - ref[0].float()).abs()
-    assert diff[:, :, :32].max().item() <= 5e-2 and diff[:, :, 32:].max().item() <= 1e-2
+    assert diff.max().item() <= 1e-2, diff.max().item()
     rq, rk, rv = R.int8_bwd(dO, ref[2], ref[5], ref[3], km, ref[6], ref[4], ref[7], ref[0], ref[1],
                             causal=True)
     for name, a, b in (("dq", qc.grad, rq), ("dk", kc.grad, rk), ("dv", vc.grad, rv)):

@@ -95,9 +95,11 @@ def test_cached_decode_vs_oracle(lib, causal, sq, pv):
     assert err <= 1e-2, err
     lerr = (lse.float().cpu() - ref[1].float()).abs()
     assert (lerr <= 2 * 2.0 ** -10 * ref[1].float().abs() + 1e-3).all(), lerr.max().item()
-    if causal:   # the last query keeps every key: its row equals the non-causal one bit for bit
+    if causal:   # the last query keeps every key: its row is the non-causal one (the diagonal tile's
+        # P_i8 follows the reference's literal chain, the non-causal kernel's 127 exp2(S - rm): the
+        # same indices up to last-bit exponential differences)
         On, _ = attention_int8_cached(q.cuda(), kv, causal=False)
-        assert torch.equal(O[:, :, -1], On[:, :, -1])
+        assert (O[:, :, -1].float() - On[:, :, -1].float()).abs().max().item() <= 5e-3
 
 
 @pytest.mark.gpu
