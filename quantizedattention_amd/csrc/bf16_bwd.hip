@@ -80,12 +80,6 @@ enum B16Role { B16_DV = 0, B16_DK = 1, B16_DQ = 2, B16_DKV = 3 };
 #ifndef QA_B16_DV_OCC
 #define QA_B16_DV_OCC 2
 #endif
-#ifndef QA_B16_SCHED
-#define QA_B16_SCHED 0   // fused dK+dV: explicit MFMA / VALU interleave, bit 1 P wave, bit 2 dS wave
-#endif
-#ifndef QA_B16_WS_ST
-#define QA_B16_WS_ST 1   // dS record stores: 1 = 2 x b128 after a half-wave swap, 0 = 4 x b64, 2 = none (timing)
-#endif
 #ifndef QA_B16_DMA_P
 #define QA_B16_DMA_P 1   // fused dK+dV: only the P waves issue the ring DMA (dS waves never wait on vmcnt)
 #endif
@@ -481,13 +475,13 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
   float X[16];
   // an active dS wave of the WS kernel ends each step with its record stores, younger than the
   // DMA of tile t+1: they may stay in flight across the barrier
-  const bool st_wave = WS && !pwave && active && QA_B16_WS_ST != 2;
+  const bool st_wave = WS && !pwave && active;
   auto ring = [&](auto SLc, int t) {
     static_assert(G::NSLOT == 3, "vmcnt counts below assume a 3-slot ring");
     if (G::DMA_WAVES == 4 && !pwave) {
       // no ring DMA in this wave: its record stores stay in flight
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else if (st_wave) ring_wait_barrier<QA_B16_WS_ST == 1 ? 2 : 4>();            // tile t+1 landed, P(t) written; slot t-1 free
+    } else if (st_wave) ring_wait_barrier<2>();            // tile t+1 landed, P(t) written; slot t-1 free
     else ring_wait_barrier<0>();
     dma.issue(smem_lds + ((decltype(SLc)::value + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
               min(t + G::NSLOT - 1, t1 - 1), lane);
@@ -536,17 +530,6 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
       operand(X, op);
       accumulate(SLc, op);                   // dV += dO^T P(t)
       pvals(NXc, min(t + 1, t1 - 1), sa, pbuf(t + 1));
-#if QA_B16_SCHED & 1
-      // LDS reads first, the 8 S MFMAs, then each dV MFMA followed by a share of the P VALU
-      __builtin_amdgcn_sched_group_barrier(0x100, 32, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, G::NKS, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-#pragma unroll
-      for (int i = 0; i < 2 * G::NDB; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-      }
-#endif
     };
     if (nt > 0) {
       pvals(I0{}, t0, sprod(I0{}), pbuf(t0));
@@ -595,7 +578,6 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
         if (active) {
           char* r = reinterpret_cast<char*>(ws) +
                     (((long)bh * (Ny / 32) + t) * (Sx / 32) + x0 / 32) * 2048 + c32 * 64;
-#if QA_B16_WS_ST == 1
           // one permlane32_swap per word pair: the h=0 lane gets queries 0-15 of its key row, the
           // h=1 lane queries 16-31; each writes 32 contiguous bytes (two b128 stores)
           const v4u w0 = __builtin_bit_cast(v4u, op[0]), w1 = __builtin_bit_cast(v4u, op[1]);
@@ -608,24 +590,8 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
           }
           *reinterpret_cast<v4u*>(r + 32 * h) = v4u{lo[0], lo[1], hi[0], hi[1]};
           *reinterpret_cast<v4u*>(r + 32 * h + 16) = v4u{lo[2], lo[3], hi[2], hi[3]};
-#elif QA_B16_WS_ST == 0
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const v4u w = __builtin_bit_cast(v4u, op[g >> 1]);
-            *reinterpret_cast<v2u*>(r + 16 * g + 8 * h) = v2u{w[2 * (g & 1)], w[2 * (g & 1) + 1]};
-          }
-#endif
         }
       }
-#if QA_B16_SCHED & 2
-      // LDS reads first, then the dP MFMAs of tile t+1 each followed by a share of the dS(t) VALU
-      __builtin_amdgcn_sched_group_barrier(0x100, 36, 0);
-#pragma unroll
-      for (int i = 0; i < G::NKS; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-      }
-#endif
     };
     if (nt > 0) {
       pa = dprod(I0{});

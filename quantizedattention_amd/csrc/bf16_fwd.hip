@@ -24,12 +24,6 @@
 
 #include "common.h"
 
-#ifndef QA_BF_AB
-#define QA_BF_AB 0
-#endif
-#ifndef QA_BF_MUNPACK
-#define QA_BF_MUNPACK 0
-#endif
 
 namespace qattn {
 
@@ -164,20 +158,6 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
   v8bf ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
-#if QA_BF_MUNPACK
-  // Widening on the matrix core: C = Sel.B with Sel[i][k] = (i == (k&3) + 8((k&7)>>2) + 4(k>>3))
-  // returns, in registers 0..7 of every lane, the lane's own eight 16-bit B elements as exact fp32
-  // (1*x + 0s), in element order.  Replaces the VALU unpack (shift / mask, or v_cvt_f32_f16) of
-  // every packed pair; the VALU is this kernel's bottleneck, the MFMA pipe has room.
-  v8h sel_h;
-  v8bf sel_b;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const bool one = c32 == (e & 3) + 8 * (e >> 2) + 4 * h;
-    sel_h[e] = one ? (_Float16)1.0f : (_Float16)0.0f;
-    sel_b[e] = one ? (__bf16)1.0f : (__bf16)0.0f;
-  }
-#endif
 
   // ring slots are compile-time constants (the tile loop is unrolled by NSLOT) so every LDS
   // address is a lane-constant VGPR plus an instruction offset
@@ -202,24 +182,12 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
   };
   const float inf = INFINITY;
   auto phase_a = [&](Sub& x, int t, int u, const v16f& acc) {
-#if QA_BF_MUNPACK
-    v4u w;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) w[j / 2] = pk_f16(acc[8 * u + j], acc[8 * u + j + 1]);
-    const v16f f = mfma_f16(sel_h, __builtin_bit_cast(v8h, w), v16f{});
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) w[j / 2] = pk_bf16(f[j], f[j + 1]);
-    const v16f sb = mfma_bf16(sel_b, __builtin_bit_cast(v8bf, w), v16f{});
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x.s[j] = sb[j];
-#else
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       const unsigned hh = pk_f16(acc[8 * u + j], acc[8 * u + j + 1]);
       const v2h p = __builtin_bit_cast(v2h, hh);
       rne2((float)p[0], (float)p[1], x.s[j], x.s[j + 1]);
     }
-#endif
     const int key_t0 = t * C::KT + 16 * u;
     if (CAUSAL && key_t0 + 15 >= q0) {
 #pragma unroll
@@ -251,17 +219,6 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
     nm = (x.M2 >= thr && nm != 0.f) ? dbl : nm;
     // P = bf16(exp2(bf16(bf16(S*qks) - nm))).  Scalar fp32 on purpose: v_pk_*_f32 issue through
     // the matrix pipe and stall ~38 cycles behind the co-resident wave's MFMAs (tools/ubench).
-#if QA_BF_MUNPACK
-    v4u w;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) w[j / 2] = pk_bf16(x.s[j] * qks, x.s[j + 1] * qks);
-    const v16f a = mfma_bf16(sel_b, __builtin_bit_cast(v8bf, w), v16f{});
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) w[j / 2] = pk_bf16(a[j] - nm, a[j + 1] - nm);
-    const v16f e = mfma_bf16(sel_b, __builtin_bit_cast(v8bf, w), v16f{});
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) x.pk[j / 2] = pk_bf16(exp2_f32(e[j]), exp2_f32(e[j + 1]));
-#else
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       float a, b;
@@ -269,7 +226,6 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
       rne2(a - nm, b - nm, a, b);
       x.pk[j / 2] = pk_bf16(exp2_f32(a), exp2_f32(b));
     }
-#endif
     x.r = rne1(exp2_f32(rne1(m - nm)));                              // bf16:276
     m = nm;
   };
@@ -283,10 +239,6 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
       for (int i = 0; i < 16; ++i) lacc[i] = lacc[i] * x.r;
     }
     const v8bf pb8 = __builtin_bit_cast(v8bf, x.pk);
-#if QA_BF_AB == 2   // timing: no P.V / l products
-    lacc[u] += __builtin_bit_cast(float, x.pk[0]);
-    return;
-#endif
     lacc = mfma_bf16(ones, pb8, lacc);                               // l = l*r + sum P   (bf16:279)
     const char* vl = smem + decltype(SLc)::value * C::SLOT;
 #pragma unroll
@@ -312,19 +264,10 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
     {
       const v16f nacc = qk(NXc);
       Sub x0, x1;
-#if QA_BF_AB == 1   // timing skeleton: no softmax
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        x0.pk[j] = pk_bf16(acc[2 * j], acc[2 * j + 1]);
-        x1.pk[j] = pk_bf16(acc[8 + 2 * j], acc[9 + 2 * j]);
-      }
-      x0.r = x1.r = 1.0f;
-#else
       phase_a(x0, t, 0, acc);
       phase_a(x1, t, 1, acc);
       phase_b(x0);
       phase_b(x1);
-#endif
       phase_c(SLc, x0, 0);
       phase_c(SLc, x1, 1);
       acc = nacc;

@@ -173,9 +173,6 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #define QA_DKV_STAGGER 1
 #endif
 // cache policy of the dS record stores (builtin aux: 2 = nt, 16 = sc1)
-#ifndef QA_WS_STORE_AUX
-#define QA_WS_STORE_AUX 0
-#endif
 
 
 template <int D, int ROLE>
@@ -417,18 +414,6 @@ void int8_bwd_kernel(
   // per-tile quantisation of X into the two bf16 B operands, scaled by so (the other operand's
   // per-tile scale)
   auto quantise = [&](const float* X, float so, v8bf* op) {
-#if defined(QA_DKV_AB)   // timing ablation only (wrong results): no quantisation arithmetic
-    if (X != nullptr) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        v4u w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = pk_bf16(X[8 * s2 + 2 * j], X[8 * s2 + 2 * j + 1]);
-        op[s2] = __builtin_bit_cast(v8bf, w);
-      }
-      return;
-    }
-#endif
     const float xmax = wave_max_dpp(max16_abs3(X));
     const float sx = xmax * (1.0f / 127.0f);
     const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
@@ -498,7 +483,7 @@ void int8_bwd_kernel(
       const int nqt = Smod / 32, nkt = Sx / 32;
       const unsigned rel = (unsigned)(t * nkt + x0 / 32);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, bytes), ws_rsrc, 16 * lane,
-                                             (int)(rel * 1024u), QA_WS_STORE_AUX);
+                                             (int)(rel * 1024u), 0);
       (void)nqt;
       if (lane == 0) sds_lds[wave * nt + t] = sx;   // written out after the loop
     }
@@ -545,9 +530,6 @@ void int8_bwd_kernel(
       quantise_ds(dS, t0, opS);
       quantise(P, so_p(t0), opP);
     }
-#if QA_DKV_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
     for (int t = t0; t < nt; ++t) {
       // tile t+1 landed: younger than its DMA are the workspace stores of tile t-1, the DMA of
       // tile t+2 and the stores of tile t
@@ -648,11 +630,7 @@ struct DqwCfg {
   static constexpr int WAVES = QA_DQW_WAVES;
   static constexpr int T16 = 64 * D;               // bf16 k image of a 32-key tile (L2-resident)
   static constexpr int NSLOT = 4;                  // k image ring: 3 tiles ahead
-#ifdef QA_DQW_RSLOT
-  static constexpr int RSLOT = QA_DQW_RSLOT;
-#else
   static constexpr int RSLOT = WAVES >= 16 ? 4 : WAVES == 8 ? 5 : 10;   // record ring (HBM stream)
-#endif
   static constexpr int REC = WAVES * 1024;         // the waves' dS records of one tile
   static constexpr int RBASE = NSLOT * T16;
   static constexpr int NP16 = T16 / 1024;
