@@ -138,6 +138,18 @@ int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const void* q_i8,
                            void* dq, void* dk, void* dv, void* ws, long bh, long sq_tok, long sk_tok,
                            int group, int causal, int head_dim, float qks, float sms, void* stream);
 
+/* qattn_int8_attn_bwd_ws in chunks of kv_chunk key/value heads (each with its group query heads):
+ * dK+dV then dQ per chunk, every chunk re-using the same ws, which must hold
+ * qattn_int8_bwd_ws_bytes(kv_chunk * group, sq_tok, sk_tok) bytes.  Bit-identical to
+ * qattn_int8_attn_bwd_ws; a chunk's records can stay in the Infinity Cache between the two passes.
+ * Returns 1 for ws == NULL or kv_chunk < 1. */
+int qattn_int8_attn_bwd_wsc(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
+                            const void* k_i8, const void* sk, const void* v_i8, const void* sv,
+                            const void* LD, const void* q_bf, const void* k_bf, const void* dO_bf,
+                            void* dq, void* dk, void* dv, void* ws, long kv_chunk, long bh,
+                            long sq_tok, long sk_tok, int group, int causal, int head_dim, float qks,
+                            float sms, void* stream);
+
 /* The two parts of qattn_int8_attn_bwd_ws (square, ungrouped, non-causal), launchable alone:
  * dK + dV writing the dS workspace, then dQ reading it. */
 int qattn_int8_bwd_dkdv_ws(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,

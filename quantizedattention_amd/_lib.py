@@ -37,6 +37,8 @@ SIGNATURES = {
     "qattn_int8_attn_bwd_ws": [_vp] * 16 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                              _c_float, _vp],
     "qattn_int8_bwd_ws_bytes": [_c_long, _c_long, _c_long],
+    "qattn_int8_attn_bwd_wsc": [_vp] * 16 + [_c_long, _c_long, _c_long, _c_long, _c_int, _c_int, _c_int,
+                                              _c_float, _c_float, _vp],
     "qattn_int8_bwd_dkdv_ws": [_vp] * 14 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_int8_bwd_dq_ws": [_vp] * 4 + [_c_long, _c_long, _c_int, _c_float, _vp],
     "qattn_int8_bwd_prep": [_vp] * 7 + [_c_long, _c_long, _c_int, _vp],
@@ -113,6 +115,25 @@ def load(path: os.PathLike | None = None) -> ctypes.CDLL:
         fn.restype = RESTYPES.get(name, ctypes.c_int)
     _lib = lib
     return lib
+
+
+_ops_loaded = False
+
+
+def load_ops() -> None:
+    """Load (once) libqattn_torch.so, the TORCH_LIBRARY(qattn) operators (csrc/torch/qattn_ops.cpp),
+    after libqattn.so whose C-ABI it calls; raises if it is absent or stale."""
+    global _ops_loaded
+    if _ops_loaded:
+        return
+    load()
+    p = _PKG / "libqattn_torch.so"
+    if not p.exists():
+        raise QAttnError(f"{p} not found: build it with `python -m quantizedattention_amd.build` "
+                         "(the qattn:: operators have no Python fallback)")
+    import torch
+    torch.ops.load_library(str(p))
+    _ops_loaded = True
 
 
 def load_dev() -> ctypes.CDLL:

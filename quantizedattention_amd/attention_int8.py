@@ -133,14 +133,29 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
 # dP, P and dS (qattn_int8_attn_bwd_ws); larger problems recompute (qattn_int8_attn_bwd_ex).  The
 # results are bit-identical either way.  1 B per score + 4 B per 32x32 tile: 2.2 GB at (4,32,4096).
 WS_MAX_BYTES = int(os.environ.get("QATTN_BWD_WS_MAX", 64 << 30))
+# Key/value heads per chunk of the record backward (qattn_int8_attn_bwd_wsc): dK+dV then dQ per
+# chunk, one chunk-sized workspace re-used by every chunk; 0: one pass over all heads; unset: auto
+# (non-causal: chunks of >= 512 dK+dV workgroups, two per CU, measured 2-4 % faster than one pass
+# at config 3 with a quarter of the workspace; causal: one pass, since a causal chunk's uneven
+# workgroups leave a longer tail per launch, measured 10-170 % slower in chunks).
+WS_CHUNK = os.environ.get("QATTN_BWD_WS_CHUNK")
+
+
+def _ws_chunk(chunk, causal, bkv, sk):
+    if chunk is None and WS_CHUNK is not None:
+        chunk = int(WS_CHUNK)
+    if chunk is None:
+        chunk = 0 if causal else -(-512 // max(1, sk // 256))
+    return bkv if chunk <= 0 else min(int(chunk), bkv)
 
 
 def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=None, causal=False,
-                   kv_heads=None, use_ws=None):
+                   kv_heads=None, use_ws=None, ws_chunk=None):
     """Corrected int8 backward; q_bf / k_bf: bf16 images from the forward (computed here if None).
 
     kv_heads: key/value heads (default: those of O); their token count follows from k_i8T.
-    use_ws: dQ from the dS workspace (True), by recomputation (False), or by size (None)."""
+    use_ws: dQ from the dS workspace (True), by recomputation (False), or by size (None).
+    ws_chunk: key/value heads per workspace chunk (None: WS_CHUNK / auto; 0 = all heads at once)."""
     O = O.to(torch.float16).contiguous()
     dO = dO.to(torch.float16).contiguous()
     _lib.require_gpu(dO, O, q_i8)
@@ -179,7 +194,8 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
               _lib.ptr(sk.contiguous()), _lib.ptr(v_i8), _lib.ptr(sv.contiguous()), _lib.ptr(LD),
               _lib.ptr(q_bf), _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv))
     shape = (B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms, st)
-    ws_bytes = _lib.load().qattn_int8_bwd_ws_bytes(B * H, S, Sk)
+    chunk = _ws_chunk(ws_chunk, causal, B * Hkv, Sk)
+    ws_bytes = _lib.load().qattn_int8_bwd_ws_bytes(chunk * (H // Hkv), S, Sk)
     # the records of one key/value head (its H / Hkv query heads) are addressed with 32-bit offsets
     region_ok = (H // Hkv) * (S // 32) * (Sk // 32) * 1024 < (1 << 31)
     if use_ws is None:
@@ -193,7 +209,9 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
             ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
         except torch.cuda.OutOfMemoryError:
             ws = None   # no room for the workspace: recompute dS in the dQ pass (same results)
-    if ws is not None:
+    if ws is not None and chunk < B * Hkv:
+        _lib.call("qattn_int8_attn_bwd_wsc", *common, _lib.ptr(ws), chunk, *shape)
+    elif ws is not None:
         _lib.call("qattn_int8_attn_bwd_ws", *common, _lib.ptr(ws), *shape)
     else:
         _lib.call("qattn_int8_attn_bwd_ex", *common, *shape)

@@ -17,6 +17,7 @@ INCLUDE = PKG.parent / "include"
 BUILD = PKG / "_build"
 LIB = PKG / "libqattn.so"
 DEV_LIB = PKG / "libqattn_dev.so"   # fragment-layout probes (csrc/dev): tests only, not product API
+OPS_LIB = PKG / "libqattn_torch.so"  # TORCH_LIBRARY(qattn) operators over libqattn.so (csrc/torch)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = [
@@ -47,7 +48,33 @@ def _compile(src: Path, obj: Path) -> str:
 def build(verbose: bool = True, jobs: int = 8) -> Path:
     _build_lib(sorted(CSRC.glob("*.hip")), LIB, "", verbose, jobs)
     _build_lib(sorted((CSRC / "dev").glob("*.hip")), DEV_LIB, "dev_", verbose, jobs)
+    build_torch_ops(verbose)
     return LIB
+
+
+def build_torch_ops(verbose: bool = True) -> Path:
+    """libqattn_torch.so: the C++ operator layer (csrc/torch/qattn_ops.cpp), host code only, compiled
+    against torch's headers and linked to libqattn.so (found beside it through the $ORIGIN rpath)."""
+    import torch
+    srcs = sorted((CSRC / "torch").glob("*.cpp"))
+    deps = srcs + [LIB] + list(INCLUDE.glob("*.h"))
+    if OPS_LIB.exists() and OPS_LIB.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
+        return OPS_LIB
+    tdir = Path(torch.__file__).resolve().parent
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared",
+           "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+           f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+           f"-I{tdir / 'include'}", f"-I{tdir / 'include' / 'torch' / 'csrc' / 'api' / 'include'}",
+           "-I/opt/rocm/include", f"-I{INCLUDE}", *map(str, srcs), "-o", str(OPS_LIB) + ".tmp",
+           f"-L{tdir / 'lib'}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+           f"-L{PKG}", "-lqattn", "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch operator library build failed:\n{r.stderr}")
+    os.replace(str(OPS_LIB) + ".tmp", OPS_LIB)
+    if verbose:
+        print(f"[qattn build] linked {OPS_LIB}", file=sys.stderr)
+    return OPS_LIB
 
 
 def _build_lib(srcs, lib, prefix: str, verbose: bool, jobs: int) -> None:

@@ -989,6 +989,38 @@ extern "C" int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const 
                          sms, stream, ws);
 }
 
+// qattn_int8_attn_bwd_ws over chunks of kv_chunk key/value heads (with their group query heads):
+// dK+dV of a chunk writes its records into ws, the dQ pass of the same chunk reads them, and the next
+// chunk re-uses the same ws bytes.  Every tensor is head-major and contiguous, so a chunk is a plain
+// pointer offset; results are bit-identical to the one-shot call (each head's arithmetic is
+// unchanged).  A workspace of one chunk's records can stay resident in the 256 MB Infinity Cache
+// between its write and its read, instead of a full-problem workspace streaming through HBM twice.
+extern "C" int qattn_int8_attn_bwd_wsc(const void* dO_i8, const void* sdO, const void* q_i8,
+                                       const void* sq, const void* k_i8, const void* sk,
+                                       const void* v_i8, const void* sv, const void* LD,
+                                       const void* q_bf, const void* k_bf, const void* dO_bf, void* dq,
+                                       void* dk, void* dv, void* ws, long kv_chunk, long bh,
+                                       long sq_tok, long sk_tok, int group, int causal, int head_dim,
+                                       float qks, float sms, void* stream) {
+  if (ws == nullptr || group < 1 || kv_chunk < 1 || !ws_region_fits(group, sq_tok, sk_tok)) return 1;
+  if (sq_tok % 32 != 0 || sk_tok % 32 != 0 || bh % group != 0 || (head_dim != 64 && head_dim != 128))
+    return 1;
+  const long bkv = bh / group, D = head_dim;
+  auto at = [](const void* p, long bytes) { return (void*)((const char*)p + bytes); };
+  for (long k0 = 0; k0 < bkv; k0 += kv_chunk) {
+    const long nkv = std::min(kv_chunk, bkv - k0);
+    const long qr = k0 * group * sq_tok, kr = k0 * sk_tok;   // first query / key row of the chunk
+    const int rc = int8_bwd_launch(
+        16 | 32, at(dO_i8, qr * D), at(sdO, qr / 32 * 2), at(q_i8, qr * D), at(sq, qr / 32 * 2),
+        at(k_i8, kr * D), at(sk, kr / 32 * 2), at(v_i8, kr * D), at(sv, kr / 32 * 2), at(LD, qr * 8),
+        at(q_bf, qr * D * 2), at(k_bf, kr * D * 2), at(dO_bf, qr * D * 2), at(dq, qr * D * 2),
+        at(dk, kr * D * 2), at(dv, kr * D * 2), nkv * group, sq_tok, sk_tok, group, causal, head_dim,
+        qks, sms, stream, ws);
+    if (rc != 0) return rc;
+  }
+  return 0;
+}
+
 // The two parts of qattn_int8_attn_bwd_ws, launchable alone (per-kernel timing).
 extern "C" int qattn_int8_bwd_dkdv_ws(const void* dO_i8, const void* sdO, const void* q_i8,
                                       const void* sq, const void* k_i8, const void* sk,

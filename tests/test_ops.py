@@ -93,3 +93,18 @@ def test_int8_quant_op_bit_exact(lib):
     assert torch.equal(idx.cpu(), ridx) and torch.equal(sc.cpu(), rsc)
     with pytest.raises(ValueError):
         torch.ops.qattn.int8_quant(x.cuda(), 64)
+
+
+def test_ops_are_cpp():
+    """The qattn:: schemas and their CUDA kernels come from libqattn_torch.so (TORCH_LIBRARY in
+    csrc/torch/qattn_ops.cpp), not from Python custom ops; no CPU kernel is registered."""
+    from quantizedattention_amd import _lib
+    assert (_lib._PKG / "libqattn_torch.so").exists()
+    for name in ("int8_quant", "int8_fwd", "int8_bwd", "bf16_fwd", "bf16_bwd", "jvp_fwd", "mxfp4_fwd"):
+        op = getattr(torch.ops.qattn, name).default
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(op.name(), "CUDA"), name
+        assert not torch._C._dispatch_has_kernel_for_dispatch_key(op.name(), "CPU"), name
+    with pytest.raises(NotImplementedError):
+        torch.ops.qattn.int8_quant(torch.zeros((1, 1, 32, 64), dtype=torch.float16), 32)
+    deps = open("/proc/self/maps").read()
+    assert "libqattn_torch.so" in deps and "libqattn.so" in deps
