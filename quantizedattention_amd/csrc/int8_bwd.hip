@@ -630,13 +630,19 @@ struct DqwCfg {
   static constexpr int WAVES = QA_DQW_WAVES;
   static constexpr int T16 = 64 * D;               // bf16 k image of a 32-key tile (L2-resident)
   static constexpr int NSLOT = 4;                  // k image ring: 3 tiles ahead
+#ifdef QA_DQW_RSLOT
+  static constexpr int RSLOT = QA_DQW_RSLOT;
+#else
   static constexpr int RSLOT = WAVES >= 16 ? 4 : WAVES == 8 ? 5 : 10;   // record ring (HBM stream)
+#endif
   static constexpr int REC = WAVES * 1024;         // the waves' dS records of one tile
   static constexpr int RBASE = NSLOT * T16;
   static constexpr int NP16 = T16 / 1024;
   // k image pieces per wave per tile; with more waves than pieces the extra waves re-issue a
   // piece (the same bytes to the same place), so every wave issues IPK + 1 DMAs per tile
   static constexpr int IPK = (NP16 + WAVES - 1) / WAVES;
+  // the pipelined loop reads tile t+1's record with tile t's k image: records run >= 1 tile ahead
+  static_assert(RSLOT - 1 >= NSLOT, "record ring must run ahead of the k image ring");
 };
 
 template <int D, bool CAUSAL>
@@ -721,18 +727,40 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
 
+  // the bf16 operand of tile t: its record brought into dQ order by the permutation MFMA (exact
+  // integers), scaled by s_dS * sk
+  auto make_op = [&](int t, v8bf* op) {
+    const v4i rec = *reinterpret_cast<const v4i*>(smem + W::RBASE + (t % W::RSLOT) * W::REC +
+                                                  wave * 1024 + 16 * lane);
+    const v16i x = mfma_i8(rec, perm, v16i{});   // dS_i8 in dQ order (exact integers)
+    const float c = sds_lds[wave * nkt + t] * (float)sk_lds[t];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      v4u w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = pk_bf16((float)x[8 * s + 2 * j] * c, (float)x[8 * s + 2 * j + 1] * c);
+      op[s] = __builtin_bit_cast(v8bf, w);
+    }
+  };
+
   vmem_drain();
   __syncthreads();
+  // Software-pipelined by one tile: the operand of tile t+1 (record read, permutation MFMA, 16
+  // conversions) is formed beside the 8 bf16 MFMAs of tile t, so a wave's MFMA chain does not wait
+  // on its own VALU chain.  Same operations as the unpipelined order: dq is bit-identical.
+  v8bf op[2];
+  if (active) make_op(0, op);
   for (int t = 0; t < nt; ++t) {
-    // tile t's k image landed (its record, issued earlier, too): younger than the k DMA of tile t
-    // are the record DMA issued with it and the k + record DMAs of the two iterations since
-    ring_wait_barrier<1 + (W::NSLOT - 2) * (W::IPK + 1)>();
+    // tile t's k image and tile t+1's record landed: with RSLOT - 1 = NSLOT both were issued three
+    // iterations ago, and younger than them are the k + record DMAs of the two iterations since
+    // (records more than one tile ahead of the k image: tile t's k image binds, and its
+    // iteration's record DMA is younger)
+    ring_wait_barrier<(W::RSLOT - 1 > W::NSLOT ? 1 : 0) + (W::NSLOT - 2) * (W::IPK + 1)>();
     issue_k(t + W::NSLOT - 1);
     issue_r(t + W::RSLOT - 1);
     if (active) {
       const char* kb = smem + (t % W::NSLOT) * W::T16;
-      const v4i rec = *reinterpret_cast<const v4i*>(smem + W::RBASE + (t % W::RSLOT) * W::REC +
-                                                    wave * 1024 + 16 * lane);
       v8bf ta[2 * C::NDB];
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -741,21 +769,14 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
           const char* a = kb + troff[b] + 16 * s * 2 * D;
           ta[s * C::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * 2 * D));
         }
-      const v16i x = mfma_i8(rec, perm, v16i{});   // dS_i8 in dQ order (exact integers)
-      const float c = sds_lds[wave * nkt + t] * (float)sk_lds[t];
-      v8bf op[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        v4u w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          w[j] = pk_bf16((float)x[8 * s + 2 * j] * c, (float)x[8 * s + 2 * j + 1] * c);
-        op[s] = __builtin_bit_cast(v8bf, w);
-      }
+      v8bf opn[2];
+      make_op(min(t + 1, nt - 1), opn);   // (the last iteration re-forms tile nt-1's: discarded)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int b = 0; b < C::NDB; ++b) acc[b] = mfma_bf16(ta[s * C::NDB + b], op[s], acc[b]);
+      op[0] = opn[0];
+      op[1] = opn[1];
     }
   }
   vmcnt_wait_all();
