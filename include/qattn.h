@@ -95,14 +95,6 @@ int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, const void* k_
                                 long sq_tok, long sk_tok, int group, int causal, int head_dim,
                                 float qks, void* stream);
 
-/* qattn_int8_attn_fwd_i8pv_ex on the role-split kernel (per 32-query block one P.V wave and two
- * softmax waves on one SIMD, handing P_i8 over through LDS).  Non-causal, head_dim 128 only
- * (returns 1 otherwise). */
-int qattn_int8_attn_fwd_rs_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                              const void* vt, const void* sv, void* out, void* lse, long bh,
-                              long sq_tok, long sk_tok, int group, int causal, int head_dim,
-                              float qks, void* stream);
-
 /* Backward prologue, one pass (attention_int8.py:372-374, 398): dO f16 -> dO_i8 [rows, D] + sdO f16
  * [rows/32] (same quantiser), dO_bf = bf16(dO_i8) [rows, D] (optional, NULL to skip), and LD f32x2
  * [rows] = {f32(lse), f32(f16(rowsum(dO*O)))}. */

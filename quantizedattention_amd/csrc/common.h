@@ -181,14 +181,6 @@ QA_DEVICE _Float16 fma_mix1(float a, float c, float n) {
 constexpr int KMAG_BITS = 0x4B400000;
 constexpr float KMAG = 12582912.0f;   // 1.5 * 2^23
 QA_DEVICE float kmag_scale(float c) { return __uint_as_float(__float_as_uint(c) & ~1u); }
-// The same with the MFMA's inline-constant C operand 1/(2 pi) (bits 0x3E22F983) as the seed, which
-// needs no seed registers.  Its mantissa 0x22F983 leaves room for -2292099 <= X < 6096509 in the
-// binade [1/8, 1/4) whose spacing is 2^-26, so the accumulator read as fp32 is exactly
-// ICB + X * 2^-26 (an i8 dot over D <= 128 has |X| <= 128 * 127 * 127 = 2064512):
-// X * c = f(acc) * (c * 2^26) - ICB * (c * 2^26), the second term rounded once.
-constexpr int ICB_BITS = 0x3E22F983;
-constexpr float ICB = __builtin_bit_cast(float, ICB_BITS);
-constexpr float ICB_SCALE = 67108864.0f;   // 2^26
 
 // d[j] = {f16(a[2j]*c + n), f16(a[2j+1]*c + n)} for the 16 values of a biased accumulator (the same
 // v_fma_mix rounding as fma_mix8).  `dep` must be a value the compiler computed FROM those

@@ -511,265 +511,6 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
                                           out + (head_row0 + q0) * D, lane, -KMAG * obias * inv);
 }
 
-
-// ------------------------------------------------------------------ role-split forward (PV_I8)
-// The same computation as int8_attn_fwd_kernel<D, PV_I8, false> with the work of a 32-query block
-// split over three waves that share one SIMD (waves w, w + 4, w + 8 of the workgroup):
-//   wave j      (role 0, "PV"):   O^T += dequant(V^T . P_i8^T) for every key tile: the running max,
-//                                 er = exp2(f16(rm - m)), l, the O rescale, the int8 P.V MFMAs and
-//                                 the per-tile dequantisation, and the epilogue;
-//   wave 4 + j  (role 1, even key tiles) and wave 8 + j (role 2, odd key tiles) ("softmax"):
-//                                 S^T = K . Q^T on the int8 MFMA, the tile row max rm,
-//                                 d = f16(S - rm), e = exp2(d), the row sums of e and P_i8 =
-//                                 trunc(127 e), handed to the PV wave through LDS (16 bytes of P_i8
-//                                 and {rm, sum e} per lane).
-// MI355X_MICROARCH / tools/ubench/coexec.py: two waves that each mix MFMA and VALU on one SIMD run no
-// faster than one (their issue costs add), while VALU-heavy waves beside an MFMA wave overlap; this
-// kernel moves the softmax VALU (about 90 of the ~120 vector instructions per wave-tile) into two
-// waves whose MFMA share is 4 per two tiles.
-// Schedule: one barrier per step.  At step s the softmax wave of parity s % 2 runs the first half of
-// tile s (fragment reads, QK^T, row max, d), the other one the second half of tile s - 1 (exp2, row
-// sums, P_i8, handoff write); the PV wave consumes tile s - 2.  Every wave runs the same nt + 2 steps
-// (no wave skips a barrier).  K/V ring of 8 slots, filled 4 tiles ahead by LDS-DMA (waves 0-3 issue
-// the V pieces, 4-7 the K pieces); two handoff slots.  Non-causal only (the causal extension keeps
-// int8_attn_fwd_kernel).  The accumulators start from the inline-constant bias (common.h ICB): no
-// seed registers, so the 12-wave workgroup fits 3 waves per SIMD (<= 168 VGPRs).
-template <int D>
-struct RsCfg {
-  static constexpr int BLK = 4;                 // 32-query blocks per workgroup
-  static constexpr int WAVES = 3 * BLK;
-  static constexpr int QROWS = 32 * BLK;
-  static constexpr int KT = 32;
-  static constexpr int NSLOT = 8;               // ring slots (power of two; >= PF + 3)
-  static constexpr int PF = 4;                  // tiles issued ahead
-  static constexpr int K_BYTES = KT * D;        // int8 K tile
-  static constexpr int SLOT = 2 * K_BYTES;      // + the vt image tile
-  static constexpr int RING = NSLOT * SLOT;
-  static constexpr int HB = 2048;               // handoff bytes per block and slot
-  static constexpr int HAND = 2 * BLK * HB;
-  static constexpr int NKS = D / 32, NDB = D / 32, K_CH = D / 16;
-  static constexpr float THR = 8.0f;
-  static_assert(NSLOT >= PF + 3, "a tile's V is read two steps after its K");
-  static_assert(K_BYTES / 1024 == BLK, "one K piece and one V piece per block and tile");
-};
-
-template <int D>
-__global__ __launch_bounds__(64 * RsCfg<D>::WAVES, 1) __attribute__((amdgpu_waves_per_eu(3, 3))) void int8_attn_fwd_rs_kernel(
-    const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
-    const _Float16* __restrict__ sk, const int8_t* __restrict__ vt, const _Float16* __restrict__ sv,
-    _Float16* __restrict__ out, _Float16* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks) {
-  using C = RsCfg<D>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* hand = smem + C::RING;
-  float* ck_lds = reinterpret_cast<float*>(smem + C::RING + C::HAND);   // sk * qks * 2^26
-  const int nq = (Sq + C::QROWS - 1) / C::QROWS;
-  int bh, qt;
-  xcd_remap(blockIdx.x, nq, BH, bh, qt);
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int role = wave >> 2, j = wave & 3;
-  const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const int q0 = qt * C::QROWS + 32 * j;
-  const bool active = q0 < Sq;
-  const long head_row0 = (long)bh * Sq;
-  const long kv_row0 = (long)(bh / G) * Sk;
-  const int nt = Sk / C::KT;
-  float* svq_lds = ck_lds + nt;                                        // sv / 127 * 2^26
-
-  // DMA plan: the PV waves bring V piece j of every tile, the even-tile softmax waves K piece j
-  const bool issuer = role < 2;
-  unsigned dvoff = 0, dlds = 0;
-  v4u drsrc = {0u, 0u, 0u, 0u};
-  if (role == 1) {
-    constexpr int RPI = 64 / C::K_CH;
-    const int row = j * RPI + lane / C::K_CH, p = lane % C::K_CH;
-    dvoff = row * D + 16 * (p ^ k_sw<D>(row));
-    dlds = j * 1024;
-    drsrc = make_rsrc(k_i8 + kv_row0 * D, (unsigned)Sk * D);
-  } else if (role == 0) {
-    dvoff = j * 1024 + 16 * lane;
-    dlds = C::K_BYTES + j * 1024;
-    drsrc = make_rsrc(vt + kv_row0 * D, (unsigned)Sk * D);
-  }
-  const unsigned smem_lds = lds_addr(smem);
-  auto issue = [&](int t) {
-    if (issuer)
-      dma16_buf(drsrc, dvoff, (unsigned)min(t, nt - 1) * C::K_BYTES,
-                smem_lds + (t & (C::NSLOT - 1)) * C::SLOT + dlds);
-  };
-#pragma unroll
-  for (int i = 0; i < C::PF; ++i) issue(i);
-  for (int i = tid; i < nt; i += 64 * C::WAVES) {
-    ck_lds[i] = (float)sk[kv_row0 / 32 + i] * qks * ICB_SCALE;
-    svq_lds[i] = (float)sv[kv_row0 / 32 + i] * (1.0f / 127.0f) * ICB_SCALE;
-  }
-  auto slot_of = [&](int t) -> const char* { return smem + (t & (C::NSLOT - 1)) * C::SLOT; };
-  // handoff region of tile t for this block
-  auto hand_of = [&](int t) -> char* { return hand + (t & 1) * (C::BLK * C::HB) + j * C::HB; };
-
-  v16i seed;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) seed[i] = ICB_BITS;   // folds into the MFMA's inline constant
-
-  // Both roles run nt + 2 steps with one barrier each, then one more barrier before the epilogue
-  // (separate loops, so that each role's registers are live only in its own loop).
-  if (role == 0) {
-    // ================================ PV wave: consumes tile st - 2 at step st
-    v16f o[C::NDB];
-#pragma unroll
-    for (int b = 0; b < C::NDB; ++b) o[b] = v16f{};
-    _Float16 m = (_Float16)(-INFINITY);
-    float l = 0.f;      // per-lane partial (this lane's key half)
-    float obias = 0.f;  // sum of the tile dequantisation factors (the bias of O is ICB * obias)
-    vmem_drain();
-    __syncthreads();
-    for (int st = 0; st < nt + 2; ++st) {
-      // tile st landed (the DMAs of st+1 .. st+PF-1 may be in flight); the handoff of tile st-2 and
-      // every read of slot (st+PF) % NSLOT (tile st+PF-NSLOT, consumed at step <= st-1) are complete
-      ring_wait_barrier<C::PF - 1>();
-      issue(st + C::PF);
-      const int t = st - 2;
-      if (!active || t < 0) continue;
-      const char* vs = slot_of(t) + C::K_BYTES;
-      v4i va[C::NDB];
-#pragma unroll
-      for (int b = 0; b < C::NDB; ++b) va[b] = *reinterpret_cast<const v4i*>(vs + b * 1024 + 16 * lane);
-      const char* hb = hand_of(t);
-      const v4i p = *reinterpret_cast<const v4i*>(hb + 16 * lane);
-      const v2u rr = *reinterpret_cast<const v2u*>(hb + 1024 + 8 * lane);
-      const _Float16 rm = __builtin_bit_cast(v2h, rr[0])[0];
-      const float rs = __uint_as_float(rr[1]);
-      // deferred running max (as int8_attn_fwd_kernel's sm1): moves only past THR
-      if (__ballot((float)rm > (float)m + C::THR) != 0) {
-        asm volatile("" ::: "memory");
-        const _Float16 nm = m > rm ? m : rm;
-        const float r = exp2_f32((float)(_Float16)(m - nm));
-        m = nm;
-        l *= r;
-        obias *= r;
-#pragma unroll
-        for (int b = 0; b < C::NDB; ++b) o[b] *= r;
-      }
-      const float er = exp2_f32((float)(_Float16)(rm - m));
-      const float cpv = er * svq_lds[t];
-      l = fmaf(rs, er, l);
-      // O += (ICB + X 2^-26) * (sp * sv * 2^26), two d blocks at a time (32 accumulator registers
-      // in flight: the 3-wave register budget)
-#pragma unroll
-      for (int hb2 = 0; hb2 < C::NDB; hb2 += 2) {
-        v16i pacc[2];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) pacc[b] = mfma_i8(va[hb2 + b], p, seed);
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[hb2 + b][r] = fmaf(__int_as_float(pacc[b][r]), cpv, o[hb2 + b][r]);
-      }
-      obias += cpv;
-    }
-    vmcnt_wait_all();
-    __syncthreads();   // every wave is done with the ring: its slots become the output staging area
-    if (!active) return;
-    // ---------------- epilogue: lse = fp16(m + fp16(log2 l)); O = fp16(O / l)   (int8:252-257)
-    l = pair_sum(l);
-    const long qrow = head_row0 + q0 + c32;
-    if (h == 0) lse[qrow] = (_Float16)((float)m + (float)(_Float16)log2_f32(l));
-    const float inv = 1.0f / l;
-    store_rows<D, _Float16, 1, true>(o, inv, smem + j * RowTile<D, _Float16>::BYTES,
-                                     out + (head_row0 + q0) * D, lane, -ICB * obias * inv);
-    return;
-  }
-  // ================================ softmax waves: tiles of parity par, each over two steps
-  const int par = role - 1;
-  v4i qf[C::NKS];
-  float cq = 0.f;
-  if (active) {
-    const int8_t* qrow = q_i8 + (head_row0 + q0 + c32) * D + 16 * h;
-#pragma unroll
-    for (int s = 0; s < C::NKS; ++s) qf[s] = *reinterpret_cast<const v4i*>(qrow + 32 * s);
-    cq = (float)sq[(head_row0 + q0) / 32];
-  }
-  int koff[C::NKS];
-#pragma unroll
-  for (int s = 0; s < C::NKS; ++s) koff[s] = c32 * D + 16 * ((2 * s + h) ^ k_sw<D>(c32));
-  v2h d[8];
-  _Float16 rm_keep = (_Float16)0.0f;
-  vmem_drain();
-  __syncthreads();
-  for (int st = 0; st < nt + 2; ++st) {
-    ring_wait_barrier<C::PF - 1>();
-    issue(st + C::PF);
-    if (!active) continue;
-    if (st < nt && (st & 1) == par) {
-      // first half of tile st: S^T, row max, d = f16(S - rm)
-      const char* kl = slot_of(st);
-      v4i kf[C::NKS];
-#pragma unroll
-      for (int s = 0; s < C::NKS; ++s) kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s]);
-      v16i acc = mfma_i8(kf[0], qf[0], seed);
-#pragma unroll
-      for (int s = 1; s < C::NKS; ++s) acc = mfma_i8(kf[s], qf[s], acc);
-      int mx = imax3(acc[0], acc[1], acc[2]);
-      mx = imax3(mx, acc[3], acc[4]);
-      mx = imax3(mx, acc[5], acc[6]);
-      mx = imax3(mx, acc[7], acc[8]);
-      mx = imax3(mx, acc[9], acc[10]);
-      mx = imax3(mx, acc[11], acc[12]);
-      mx = imax3(mx, acc[13], acc[14]);
-      mx = max(mx, acc[15]);
-      {
-        auto r = __builtin_amdgcn_permlane32_swap((unsigned)mx, (unsigned)mx, false, false);
-        mx = max((int)r[0], (int)r[1]);
-      }
-      // S = f16(X * c) on the biased accumulator, c = sq * sk * qks (int8:200-203)
-      const float c = cq * ck_lds[st];
-      const float nb = -ICB * c;
-      const _Float16 rm = fma_mix1(__int_as_float(mx), c, nb);
-      v2h s2[8];
-      fma_mix16_after(acc, c, nb, mx, s2);
-      const v2h rm2 = {rm, rm};
-#pragma unroll
-      for (int q = 0; q < 8; ++q) d[q] = s2[q] - rm2;   // f16(S - rm)  (int8:211, 232-236)
-      rm_keep = rm;
-    } else if (st >= 1 && st - 1 < nt && ((st - 1) & 1) == par) {
-      // second half of tile st-1: e = exp2(d), row sums, P_i8 = trunc(127 e); handoff
-      v2h e[8];
-      exp2_pk4(&d[0], &e[0]);
-      exp2_pk4(&d[4], &e[4]);
-      const v2h sm = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
-      const float rs = pk_hsum(sm);
-      const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
-      unsigned y[8];
-      p_index8(e, k127, y);
-      char* hb = hand_of(st - 1);
-      *reinterpret_cast<v4i*>(hb + 16 * lane) = pack_p_index(y);
-      const v2h rmv = {rm_keep, rm_keep};
-      *reinterpret_cast<v2u*>(hb + 1024 + 8 * lane) =
-          v2u{__builtin_bit_cast(unsigned, rmv), __float_as_uint(rs)};
-    }
-  }
-  vmcnt_wait_all();
-  __syncthreads();
-}
-
-template <int D>
-static int launch_fwd_rs(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                         const void* vt, const void* sv, void* out, void* lse, long bh, long sq_tok,
-                         long sk_tok, int group, float qks, hipStream_t st) {
-  using C = RsCfg<D>;
-  static_assert(C::BLK * RowTile<D, _Float16>::BYTES <= C::RING, "epilogue staging fits the ring");
-  const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
-  const int lds = C::RING + C::HAND + (int)(((sk_tok / 32) * 8 + 15) / 16 * 16);
-  if (lds > 160 * 1024) return 1;
-  hipFuncSetAttribute((const void*)int8_attn_fwd_rs_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      lds);
-  hipLaunchKernelGGL((int8_attn_fwd_rs_kernel<D>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds, st,
-                     (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
-                     (const int8_t*)vt, (const _Float16*)sv, (_Float16*)out, (_Float16*)lse, (int)bh,
-                     (int)sq_tok, (int)sk_tok, group, qks);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
 template <int D, int PV, bool CAUSAL>
 static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
                       const void* vop, const void* sv, void* out, void* lse, long bh, long sq_tok,
@@ -830,19 +571,4 @@ extern "C" int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, con
   if (sv == nullptr) return 1;
   return fwd_dispatch<PV_I8>(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, causal,
                              head_dim, qks, stream);
-}
-
-// The role-split kernel (non-causal, head_dim 128; int8_attn_fwd_rs_kernel) with the arguments of
-// qattn_int8_attn_fwd_i8pv_ex; returns 1 for the shapes it does not cover.
-extern "C" int qattn_int8_attn_fwd_rs_ex(const void* q_i8, const void* sq, const void* k_i8,
-                                         const void* sk, const void* vt, const void* sv, void* out,
-                                         void* lse, long bh, long sq_tok, long sk_tok, int group,
-                                         int causal, int head_dim, float qks, void* stream) {
-  if (sv == nullptr || causal != 0 || head_dim != 128 || sq_tok % 32 != 0 || sk_tok % 32 != 0 ||
-      group < 1 || bh % group != 0)
-    return 1;
-  if (bh == 0 || sq_tok == 0) return 0;
-  if (sk_tok == 0) return 1;
-  return launch_fwd_rs<128>(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, qks,
-                            (hipStream_t)stream);
 }
