@@ -247,6 +247,22 @@ def other_configs(n):
     out["cfg4_int8_fwd_bwd_1gpu"] = {"shape": [B, H, S, D], "ms": t, "TOPs": flop / (t * 1e-3) / 1e12,
                                      "frac_of_int8_peak": flop / (t * 1e-3) / PEAK_I8}
     del q, k, v, dO
+    # a decoding step against the int8 key/value cache -- 32 new queries per head,
+    # 8 key/value heads shared by 32 query heads, 8192 cached tokens (kv_cache: grouped heads in
+    # one workgroup, key splits merged); HBM-bound by the cache read
+    from quantizedattention_amd.kv_cache import attention_int8_cached, quantize_kv
+    B, Hq, Hkv, Sq, Sk, D = 8, 32, 8, 32, 8192, 128
+    kc, vc = (torch.randn((B, Hkv, Sk, D), device=dev, generator=g).half() for _ in range(2))
+    qd = torch.randn((B, Hq, Sq, D), device=dev, generator=g).half()
+    kv = quantize_kv(kc, vc)
+    t = event_time(lambda: attention_int8_cached(qd, kv), n)
+    cache = 2 * B * Hkv * Sk * D + 2 * 2 * B * Hkv * Sk // 32
+    out["n3_int8_kv_decode"] = {"shape": {"B": B, "Hq": Hq, "Hkv": Hkv, "Sq": Sq, "Sk": Sk, "D": D},
+                                "ms": t, "cache_bytes": cache,
+                                "cache_TBps": cache / (t * 1e-3) / 1e12,
+                                "frac_of_hbm_peak": cache / (t * 1e-3) / PEAK_HBM,
+                                "TOPs": 4.0 * B * Hq * Sq * Sk * D / (t * 1e-3) / 1e12}
+    del kc, vc, qd, kv
     B, H, S, D = 2, 16, 2048, 128
     x = [torch.randn((B, H, S, D), device=dev, generator=g).bfloat16() for _ in range(6)]
     t = event_time(lambda: helion_attention_jvp_forward_fp32(*x), n)

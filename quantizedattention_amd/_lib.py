@@ -32,6 +32,9 @@ SIGNATURES = {
     "qattn_int8_attn_fwd_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_i8pv_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                  _vp],
+    "qattn_int8_attn_fwd_split": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
+                                               _vp],
+    "qattn_int8_split_combine": [_vp] * 4 + [_c_long, _c_int, _c_int, _vp],
     "qattn_int8_attn_bwd_ex": [_vp] * 15 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                              _c_float, _vp],
     "qattn_int8_attn_bwd_ws": [_vp] * 16 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,

@@ -179,15 +179,22 @@ struct SmTile {
 // scores are excluded (P = 0).  The reference has neither (its int8 path is square, ungrouped and
 // non-causal, int8:122-127, 344); these are extensions.
 // vop: PV_F16 the vdq image f16 [BHkv*Sk, D]; PV_I8 the vt image (qattn_int8_quant_vt).
+// SPLIT (key-split decoding, PV_I8 non-causal): workgroup (x, y) covers keys [y ks, y ks + ks) of
+// its query rows and writes the un-normalised partial state instead of O: through `out`, opart f32
+// [split][BH*Sq][D] = O_s with the accumulator bias removed; through `lse`, ml f32x2 [split][BH*Sq]
+// = {m_s, l_s} (running max, row sum); int8_split_combine_kernel merges the splits.  (The two
+// outputs reuse the pointer arguments and ks the causal offset qoff: the causal instantiations are
+// at the SGPR limit, one more kernel argument pushes their buffer descriptors into VGPRs.)
 // (the causal PV_F16 kernel's diagonal masking does not fit 168 VGPRs: 2 waves per SIMD)
 template <int D, int PV, bool CAUSAL>
 constexpr int fwd_wps() { return CAUSAL ? 2 : Int8FwdCfg<D, PV>::WPS; }
-template <int D, int PV, bool CAUSAL>
+template <int D, int PV, bool CAUSAL, bool SPLIT = false>
 __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CAUSAL>())) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
     const _Float16* __restrict__ sk, const void* __restrict__ vop, const _Float16* __restrict__ sv,
     _Float16* __restrict__ out, _Float16* __restrict__ lse, int BH, int Sq, int Sk, int G, int qoff,
     float qks) {
+  static_assert(!SPLIT || (PV == PV_I8 && !CAUSAL), "key splits: int8 P.V, non-causal");
   using C = Int8FwdCfg<D, PV>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per-tile scales: ck = sk * qks (f32); PV_I8 also sv / 127 (f32)
@@ -204,18 +211,22 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   const int q0 = qt * C::QROWS + wave * 32;
   const bool active = q0 < Sq;
   const long head_row0 = (long)bh * Sq;           // this head's query rows
-  const long kv_row0 = (long)(bh / G) * Sk;       // its key/value head's rows
+  const int split = SPLIT ? (int)__builtin_amdgcn_readfirstlane(blockIdx.y) : 0;
+  const int ks = qoff;                             // SPLIT (non-causal): keys per split
+  const int k0 = SPLIT ? split * ks : 0;           // first key of this workgroup's key range
+  const int nk = SPLIT ? min(ks, Sk - k0) : Sk;    // its keys
+  const long kv_row0 = (long)(bh / G) * Sk + k0;  // its key/value head's rows
   const int8_t* kbase = k_i8 + kv_row0 * D;
   const void* vbase = PV == PV_F16
       ? (const void*)(reinterpret_cast<const _Float16*>(vop) + kv_row0 * D)
       : (const void*)(reinterpret_cast<const int8_t*>(vop) + kv_row0 * D);
   // causal: key tiles past the workgroup's last query are masked for all of its rows
   const int nt = CAUSAL ? min(Sk / C::KT, (qt * C::QROWS + C::QROWS + qoff + C::KT - 1) / C::KT)
-                        : Sk / C::KT;
+                        : nk / C::KT;
   float* svq_lds = ck_lds + nt;
 
   DmaPlan<D, PV> dma;
-  dma.init(wave, lane, Sk, kbase, vbase);
+  dma.init(wave, lane, Sk - k0, kbase, vbase);   // (the range bound only: reads stay in nk)
   const unsigned smem_lds = lds_addr(smem);
   dma.issue(smem_lds, 0);
   dma.issue(smem_lds + 1 * C::SLOT, min(1, nt - 1));
@@ -502,6 +513,14 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   __syncthreads();   // every wave is done with the ring: its slots become the output staging area
 
   if (!active) return;
+  if constexpr (SPLIT) {   // the partial state of this key range: {m, l} and O - KMAG * obias
+    l = pair_sum(l);
+    const long prow = ((long)split * BH + bh) * Sq + q0;
+    if (h == 0) reinterpret_cast<float2*>(lse)[prow + c32] = float2{(float)m, l};
+    store_rows<D, float, 2, true>(o, 1.0f, smem + wave * RowTile<D, float, 2>::BYTES,
+                                  reinterpret_cast<float*>(out) + prow * D, lane, -KMAG * obias);
+    return;
+  }
   // ---------------- epilogue: lse = fp16(m + fp16(log2 l)); O = fp16(O / l)   (int8:252-257)
   l = pair_sum(l);
   const long qrow = head_row0 + q0 + c32;
@@ -524,6 +543,62 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
                      (const int8_t*)k_i8, (const _Float16*)sk, vop, (const _Float16*)sv,
                      (_Float16*)out, (_Float16*)lse, (int)bh, (int)sq_tok, (int)sk_tok, group, qoff, qks);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Merge of the key splits (flash-decoding): per row M = max_s m_s, w_s = exp2(m_s - M),
+// L = sum_s w_s l_s, O = f16(sum_s w_s O_s / L), lse = f16(M + f16(log2 L)) (int8:252-257 on the merged
+// state).  One thread per 8 columns of a row.
+template <int D>
+__global__ __launch_bounds__(256) void int8_split_combine_kernel(const float* __restrict__ opart,
+                                                                 const float2* __restrict__ ml,
+                                                                 _Float16* __restrict__ out,
+                                                                 _Float16* __restrict__ lse, long rows,
+                                                                 int nsplit) {
+  constexpr int TPR = D / 8;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long row = gid / TPR;
+  const int c = (int)(gid % TPR);
+  if (row >= rows) return;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[s * rows + row].x);
+  float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < nsplit; ++s) {
+    const float2 v = ml[s * rows + row];
+    const float w = exp2_f32(v.x - M);
+    L = fmaf(w, v.y, L);
+    const float* src = opart + ((long)s * rows + row) * D + 8 * c;
+    const v4f a = *reinterpret_cast<const v4f*>(src);
+    const v4f b = *reinterpret_cast<const v4f*>(src + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i] = fmaf(w, a[i], acc[i]);
+      acc[4 + i] = fmaf(w, b[i], acc[4 + i]);
+    }
+  }
+  const float inv = 1.0f / L;
+  v8h o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (_Float16)(acc[i] * inv);
+  *reinterpret_cast<v8h*>(out + row * D + 8 * c) = o;
+  if (c == 0) lse[row] = (_Float16)(M + (float)(_Float16)log2_f32(L));
+}
+
+template <int D>
+static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
+                            const void* vt, const void* sv, void* opart, void* ml, long bh, long sq_tok,
+                            long sk_tok, int group, int ks, float qks, hipStream_t st) {
+  using C = Int8FwdCfg<D, PV_I8>;
+  static_assert(C::WAVES * RowTile<D, float, 2>::BYTES <= C::RING, "partial-state staging fits the ring");
+  const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
+  const int nsplit = (int)((sk_tok + ks - 1) / ks);
+  const int lds = C::RING + (int)(((ks / 32) * 8 + 15) / 16 * 16);
+  hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<D, PV_I8, false, true>,
+                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV_I8, false, true>), dim3((unsigned)(nq * bh), (unsigned)nsplit),
+                     dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
+                     (const int8_t*)k_i8, (const _Float16*)sk, vt, (const _Float16*)sv, (_Float16*)opart,
+                     (_Float16*)ml, (int)bh, (int)sq_tok, (int)sk_tok, group, ks, qks);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -571,4 +646,40 @@ extern "C" int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, con
   if (sv == nullptr) return 1;
   return fwd_dispatch<PV_I8>(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, causal,
                              head_dim, qks, stream);
+}
+
+// Key-split (flash-decoding) form of qattn_int8_attn_fwd_i8pv_ex for short query blocks against
+// long key ranges (the int8 key/value cache), non-causal: every workgroup covers
+// keys_per_split keys (a multiple of 32) of its query rows and writes the partial state
+//   opart f32 [nsplit][bh*sq_tok][D] and ml f32x2 [nsplit][bh*sq_tok] = {m_s, l_s},
+// nsplit = ceil(sk_tok / keys_per_split); qattn_int8_split_combine merges it into out / lse.
+// head_dim 128 only (the D = 64 instantiation exceeds the SGPR budget of its buffer descriptors).
+extern "C" int qattn_int8_attn_fwd_split(const void* q_i8, const void* sq, const void* k_i8,
+                                         const void* sk, const void* vt, const void* sv, void* opart,
+                                         void* ml, long bh, long sq_tok, long sk_tok, int group,
+                                         int keys_per_split, int head_dim, float qks, void* stream) {
+  if (sv == nullptr || opart == nullptr || ml == nullptr || sq_tok % 32 != 0 || sk_tok % 32 != 0 ||
+      group < 1 || bh % group != 0 || keys_per_split < 32 || keys_per_split % 32 != 0 ||
+      head_dim != 128)
+    return 1;
+  if (bh == 0 || sq_tok == 0) return 0;
+  if (sk_tok == 0) return 1;
+  return launch_fwd_split<128>(q_i8, sq, k_i8, sk, vt, sv, opart, ml, bh, sq_tok, sk_tok, group,
+                               keys_per_split, qks, (hipStream_t)stream);
+}
+
+extern "C" int qattn_int8_split_combine(const void* opart, const void* ml, void* out, void* lse, long rows,
+                                        int nsplit, int head_dim, void* stream) {
+  if (nsplit < 1 || (head_dim != 64 && head_dim != 128) || rows < 0) return 1;
+  if (rows == 0) return 0;
+  const long threads = rows * (head_dim / 8);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (head_dim == 128)
+    hipLaunchKernelGGL(int8_split_combine_kernel<128>, grid, dim3(256), 0, st, (const float*)opart,
+                       (const float2*)ml, (_Float16*)out, (_Float16*)lse, rows, nsplit);
+  else
+    hipLaunchKernelGGL(int8_split_combine_kernel<64>, grid, dim3(256), 0, st, (const float*)opart,
+                       (const float2*)ml, (_Float16*)out, (_Float16*)lse, rows, nsplit);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
 }

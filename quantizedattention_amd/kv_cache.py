@@ -211,7 +211,11 @@ def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False
     Hq must be a multiple of the cache's heads (grouped-query attention).  ``causal``: the Sq queries
     are the LAST Sq positions (query i keeps keys <= Sk - Sq + i), Sq <= Sk.  Returns (O fp16
     [B, Hq, Sq, D], lse fp16 [B*Hq*Sq]); without ``causal`` identical to the forward on the un-cached
-    tensors.  ``pv``: the P.V mode (default attention_int8.PV_MODE).
+    tensors (bit-identical when one key split covers the cache).  ``pv``: the P.V mode (default
+    attention_int8.PV_MODE).
+    Non-causal with the int8 P.V at head_dim 128 runs in the decoding layout (_decode_split: the
+    grouped query heads of a key/value head in one workgroup, long caches split over the keys and
+    merged); the results equal the one-pass forward's up to the merge's rounding (<= 2e-3).
     """
     from . import attention_int8
     pv = attention_int8.PV_MODE if pv is None else pv
@@ -232,6 +236,9 @@ def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False
     _lib.call("qattn_int8_quant", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), None, None, N, Sq, D, st)
     qks = float(torch.tensor(1.0 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
     mode = 2 if causal else 0          # bottom-right aligned causal mask
+    if not causal and pv != "f16" and D == 128:
+        _decode_split(q_i8, sq, kv, O, lse, B, Hq, Sq, qks, st)
+        return O, lse
     if pv == "f16":
         _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
                   _lib.ptr(kv.sk), _lib.ptr(kv.vdq()), _lib.ptr(O), _lib.ptr(lse), B * Hq, Sq, Sk,
@@ -241,3 +248,42 @@ def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False
                   _lib.ptr(kv.sk), _lib.ptr(kv.vt()), _lib.ptr(kv.sv), _lib.ptr(O), _lib.ptr(lse),
                   B * Hq, Sq, Sk, Hq // Hkv, mode, D, qks, st)
     return O, lse
+
+
+def _split_plan(bhv: int, rows: int, sk: int) -> int:
+    """Keys per split of the decoding forward: enough workgroups for two per CU (512), each split
+    at least 32 key tiles (1024 keys: a workgroup's fixed prologue / epilogue cost is worth ~20
+    tiles); sk (a multiple of 32) when one split suffices.  Measured on MI355X (tools/sweep_decode.py,
+    D = 128): (B, Hq, Hkv, Sk) = (8, 32, 8, 8192) 1024 keys 56 us (512: 72, 2048: 60, one pass
+    154); (8, 32, 32, 8192) 4096 keys 110 us (1024: 127, one pass 142); (1, 32, 8, 32768) 1024 keys
+    49 us (512: 65, 2048: 56, one pass 578)."""
+    wgs = bhv * -(-rows // 128)
+    nsplit = max(1, min(sk // 1024, -(-512 // wgs)))
+    return -(-(sk // 32) // nsplit) * 32
+
+
+def _decode_split(q_i8, sq, kv, O, lse, B, Hq, Sq, qks, st):
+    """Non-causal cached attention in the decoding layout.
+
+    * Grouped query heads share one key/value head: the G = Hq / Hkv query heads of a key/value
+      head are consecutive [Sq, D] blocks in memory, so they are run as ONE virtual head of G * Sq
+      rows against that key/value head (group 1): the G heads' query blocks sit in one workgroup
+      and read each key/value tile once (same rows, same scale blocks, same outputs).
+    * Short query blocks against long caches are split over the keys (qattn_int8_attn_fwd_split)
+      and merged (qattn_int8_split_combine), so that the grid fills the chip."""
+    _, Hkv, Sk, D = kv.shape
+    bhv, rows = B * Hkv, (Hq // Hkv) * Sq
+    ks = _split_plan(bhv, rows, Sk)
+    if ks >= Sk:
+        _lib.call("qattn_int8_attn_fwd_i8pv_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
+                  _lib.ptr(kv.sk), _lib.ptr(kv.vt()), _lib.ptr(kv.sv), _lib.ptr(O), _lib.ptr(lse),
+                  bhv, rows, Sk, 1, 0, D, qks, st)
+        return
+    nsplit = -(-Sk // ks)
+    opart = torch.empty((nsplit, bhv * rows, D), dtype=torch.float32, device=O.device)
+    ml = torch.empty((nsplit, bhv * rows, 2), dtype=torch.float32, device=O.device)
+    _lib.call("qattn_int8_attn_fwd_split", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
+              _lib.ptr(kv.sk), _lib.ptr(kv.vt()), _lib.ptr(kv.sv), _lib.ptr(opart), _lib.ptr(ml),
+              bhv, rows, Sk, 1, ks, D, qks, st)
+    _lib.call("qattn_int8_split_combine", _lib.ptr(opart), _lib.ptr(ml), _lib.ptr(O), _lib.ptr(lse),
+              bhv * rows, nsplit, D, st)

@@ -140,3 +140,44 @@ def test_cache_from_forward_outputs(lib, pv):
     kv = QuantizedKV.from_forward_outputs(out, batch=2, kv_heads=2)
     O, lse = attention_int8_cached(q, kv)
     assert torch.equal(O, out[0]) and torch.equal(lse, out[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,hq,hkv,sq,sk", [(1, 8, 2, 32, 4096), (2, 4, 4, 32, 4192), (1, 16, 2, 64, 2080)])
+def test_cached_decode_split_vs_oracle(lib, b, hq, hkv, sq, sk):
+    """Decoding layout (kv_cache._decode_split): grouped query heads run as one virtual head per
+    key/value head and long caches are split over the keys (qattn_int8_attn_fwd_split) and merged
+    (qattn_int8_split_combine).  O within the int8 bar (1e-2) of the oracle on the same inputs, lse
+    within 2 fp16 ulp; and within 2e-3 of the one-pass forward (the merge re-rounds exp2(m_s - M))."""
+    from oracle import restate as R
+    from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
+    from quantizedattention_amd.kv_cache import _split_plan, attention_int8_cached, quantize_kv
+    D = 128
+    assert _split_plan(b * hkv, (hq // hkv) * sq, sk) < sk      # the split path runs
+    q = _fp16((b, hq, sq, D), 31)
+    k = _fp16((b, hkv, sk, D), 32)
+    v = _fp16((b, hkv, sk, D), 33)
+    kv = quantize_kv(k.cuda(), v.cuda(), smooth=False)
+    O, lse = attention_int8_cached(q.cuda(), kv)
+    ref1 = helion_atten_int8_hl_dot_fwd(q.cuda(), k.cuda(), v.cuda())
+    torch.cuda.synchronize()
+    assert torch.isfinite(O).all()
+    assert (O.float() - ref1[0].float()).abs().max().item() <= 2e-3
+    G = hq // hkv
+    for h in (0, hq - 1):   # two query heads (first and last group) against the oracle
+        ref = R.int8_fwd(q[:1, h:h + 1], k[:1, h // G:h // G + 1], v[:1, h // G:h // G + 1])
+        err = (O[0, h].float().cpu() - ref[0][0, 0].float()).abs().max().item()
+        assert err <= 1e-2, (h, err)
+        lrow = lse.view(b, hq, sq)[0, h].float().cpu()
+        assert ((lrow - ref[1].float()).abs() <= 2 * 2.0 ** -10 * ref[1].float().abs() + 1e-3).all()
+
+
+def test_split_plan():
+    """Keys per split: one split when the query blocks alone fill the chip, else >= 32 key tiles."""
+    from quantizedattention_amd.kv_cache import _split_plan
+    assert _split_plan(256, 2048, 4096) == 4096          # plenty of workgroups: no split
+    ks = _split_plan(2, 128, 4096)
+    assert ks % 32 == 0 and 1024 <= ks < 4096
+    assert _split_plan(64, 128, 8192) == 1024            # 64 workgroups x 8 splits = 512
+    assert _split_plan(8, 128, 32768) == 1024            # 8 x 32 (>= 1024 keys per split)
+    assert _split_plan(256, 32, 8192) == 4096            # 256 x 2
