@@ -613,6 +613,15 @@ static int fwd_dispatch(const void* q_i8, const void* sq, const void* k_i8, cons
   if (sk_tok == 0 || (causal == 2 && sk_tok < sq_tok)) return 1;   // every query keeps a key
   const int qoff = causal == 2 ? (int)(sk_tok - sq_tok) : 0;
   hipStream_t st = (hipStream_t)stream;
+  // Non-causal grouped-query attention with short query blocks: the group's query heads are
+  // consecutive [sq_tok, D] blocks (rows, scale blocks, O and lse alike), so they run as one virtual
+  // head of group * sq_tok rows against their key/value head -- the same arithmetic per row
+  // (bit-identical), with the workgroup's waves filled and each key/value tile read once per group.
+  if (causal == 0 && group > 1 && sq_tok % Int8FwdCfg<128, PV>::QROWS != 0) {
+    sq_tok *= group;
+    bh /= group;
+    group = 1;
+  }
 #define QA_L(Dv, CV) \
   launch_fwd<Dv, PV, CV>(q_i8, sq, k_i8, sk, vop, sv, out, lse, bh, sq_tok, sk_tok, group, qoff, qks, st)
   if (head_dim == 128) return causal ? QA_L(128, true) : QA_L(128, false);
