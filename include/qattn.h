@@ -98,10 +98,10 @@ int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, const void* k_
 /* Key-split (flash-decoding) form of qattn_int8_attn_fwd_i8pv_ex, non-causal, for short query blocks
  * against long key ranges (the int8 key/value cache): each workgroup covers
  * keys_per_split keys (multiple of 32) of its query rows and writes the partial softmax state
- *   opart f32 [nsplit][bh*sq_tok][D] (un-normalised O of the key range) and
+ *   opart f16 [nsplit][bh*sq_tok][D] = O_s / l_s (the key range's normalised output) and
  *   ml f32x2 [nsplit][bh*sq_tok] = {running max m_s, row sum l_s}, nsplit = ceil(sk_tok/keys_per_split);
  * qattn_int8_split_combine merges the splits into out f16 [rows, D] and lse f16 [rows] (rows =
- * bh*sq_tok): O = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s, lse = f16(M + f16(log2 L)).
+ * bh*sq_tok): w_s = 2^(m_s - M) l_s, O = sum_s w_s opart_s / sum_s w_s, lse = f16(M + f16(log2 L)).
  * head_dim 128 only for the split forward (returns 1 otherwise). */
 int qattn_int8_attn_fwd_split(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
                               const void* vt, const void* sv, void* opart, void* ml, long bh,

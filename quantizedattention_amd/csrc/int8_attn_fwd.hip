@@ -180,9 +180,9 @@ struct SmTile {
 // non-causal, int8:122-127, 344); these are extensions.
 // vop: PV_F16 the vdq image f16 [BHkv*Sk, D]; PV_I8 the vt image (qattn_int8_quant_vt).
 // SPLIT (key-split decoding, PV_I8 non-causal): workgroup (x, y) covers keys [y ks, y ks + ks) of
-// its query rows and writes the un-normalised partial state instead of O: through `out`, opart f32
-// [split][BH*Sq][D] = O_s with the accumulator bias removed; through `lse`, ml f32x2 [split][BH*Sq]
-// = {m_s, l_s} (running max, row sum); int8_split_combine_kernel merges the splits.  (The two
+// its query rows and writes the partial state instead of O: through `out`, opart f16
+// [split][BH*Sq][D] = f16(O_s / l_s) (the split's normalised output); through `lse`, ml f32x2
+// [split][BH*Sq] = {m_s, l_s} (running max, row sum); int8_split_combine_kernel merges the splits.  (The two
 // outputs reuse the pointer arguments and ks the causal offset qoff: the causal instantiations are
 // at the SGPR limit, one more kernel argument pushes their buffer descriptors into VGPRs.)
 // (the causal PV_F16 kernel's diagonal masking does not fit 168 VGPRs: 2 waves per SIMD)
@@ -513,12 +513,13 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   __syncthreads();   // every wave is done with the ring: its slots become the output staging area
 
   if (!active) return;
-  if constexpr (SPLIT) {   // the partial state of this key range: {m, l} and O - KMAG * obias
+  if constexpr (SPLIT) {   // the partial state of this key range: {m, l} and f16(O / l)
     l = pair_sum(l);
     const long prow = ((long)split * BH + bh) * Sq + q0;
     if (h == 0) reinterpret_cast<float2*>(lse)[prow + c32] = float2{(float)m, l};
-    store_rows<D, float, 2, true>(o, 1.0f, smem + wave * RowTile<D, float, 2>::BYTES,
-                                  reinterpret_cast<float*>(out) + prow * D, lane, -KMAG * obias);
+    const float inv = 1.0f / l;
+    store_rows<D, _Float16, 1, true>(o, inv, smem + wave * RowTile<D, _Float16>::BYTES,
+                                     out + prow * D, lane, -KMAG * obias * inv);
     return;
   }
   // ---------------- epilogue: lse = fp16(m + fp16(log2 l)); O = fp16(O / l)   (int8:252-257)
@@ -546,11 +547,11 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-// Merge of the key splits (flash-decoding): per row M = max_s m_s, w_s = exp2(m_s - M),
-// L = sum_s w_s l_s, O = f16(sum_s w_s O_s / L), lse = f16(M + f16(log2 L)) (int8:252-257 on the merged
-// state).  One thread per 8 columns of a row.
+// Merge of the key splits (flash-decoding): per row M = max_s m_s, w_s = exp2(m_s - M) l_s,
+// L = sum_s w_s, O = f16(sum_s w_s Ô_s / L) with Ô_s = O_s / l_s the split's normalised output,
+// lse = f16(M + f16(log2 L)) (int8:252-257 on the merged state).  One thread per 8 columns of a row.
 template <int D>
-__global__ __launch_bounds__(256) void int8_split_combine_kernel(const float* __restrict__ opart,
+__global__ __launch_bounds__(256) void int8_split_combine_kernel(const _Float16* __restrict__ opart,
                                                                  const float2* __restrict__ ml,
                                                                  _Float16* __restrict__ out,
                                                                  _Float16* __restrict__ lse, long rows,
@@ -565,16 +566,11 @@ __global__ __launch_bounds__(256) void int8_split_combine_kernel(const float* __
   float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int s = 0; s < nsplit; ++s) {
     const float2 v = ml[s * rows + row];
-    const float w = exp2_f32(v.x - M);
-    L = fmaf(w, v.y, L);
-    const float* src = opart + ((long)s * rows + row) * D + 8 * c;
-    const v4f a = *reinterpret_cast<const v4f*>(src);
-    const v4f b = *reinterpret_cast<const v4f*>(src + 4);
+    const float w = exp2_f32(v.x - M) * v.y;
+    L += w;
+    const v8h a = *reinterpret_cast<const v8h*>(opart + ((long)s * rows + row) * D + 8 * c);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      acc[i] = fmaf(w, a[i], acc[i]);
-      acc[4 + i] = fmaf(w, b[i], acc[4 + i]);
-    }
+    for (int i = 0; i < 8; ++i) acc[i] = fmaf(w, (float)a[i], acc[i]);
   }
   const float inv = 1.0f / L;
   v8h o;
@@ -589,7 +585,6 @@ static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, 
                             const void* vt, const void* sv, void* opart, void* ml, long bh, long sq_tok,
                             long sk_tok, int group, int ks, float qks, hipStream_t st) {
   using C = Int8FwdCfg<D, PV_I8>;
-  static_assert(C::WAVES * RowTile<D, float, 2>::BYTES <= C::RING, "partial-state staging fits the ring");
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int nsplit = (int)((sk_tok + ks - 1) / ks);
   const int lds = C::RING + (int)(((ks / 32) * 8 + 15) / 16 * 16);
@@ -660,7 +655,7 @@ extern "C" int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, con
 // Key-split (flash-decoding) form of qattn_int8_attn_fwd_i8pv_ex for short query blocks against
 // long key ranges (the int8 key/value cache), non-causal: every workgroup covers
 // keys_per_split keys (a multiple of 32) of its query rows and writes the partial state
-//   opart f32 [nsplit][bh*sq_tok][D] and ml f32x2 [nsplit][bh*sq_tok] = {m_s, l_s},
+//   opart f16 [nsplit][bh*sq_tok][D] = O_s / l_s and ml f32x2 [nsplit][bh*sq_tok] = {m_s, l_s},
 // nsplit = ceil(sk_tok / keys_per_split); qattn_int8_split_combine merges it into out / lse.
 // head_dim 128 only (the D = 64 instantiation exceeds the SGPR budget of its buffer descriptors).
 extern "C" int qattn_int8_attn_fwd_split(const void* q_i8, const void* sq, const void* k_i8,
@@ -685,10 +680,10 @@ extern "C" int qattn_int8_split_combine(const void* opart, const void* ml, void*
   const dim3 grid((unsigned)((threads + 255) / 256));
   hipStream_t st = (hipStream_t)stream;
   if (head_dim == 128)
-    hipLaunchKernelGGL(int8_split_combine_kernel<128>, grid, dim3(256), 0, st, (const float*)opart,
+    hipLaunchKernelGGL(int8_split_combine_kernel<128>, grid, dim3(256), 0, st, (const _Float16*)opart,
                        (const float2*)ml, (_Float16*)out, (_Float16*)lse, rows, nsplit);
   else
-    hipLaunchKernelGGL(int8_split_combine_kernel<64>, grid, dim3(256), 0, st, (const float*)opart,
+    hipLaunchKernelGGL(int8_split_combine_kernel<64>, grid, dim3(256), 0, st, (const _Float16*)opart,
                        (const float2*)ml, (_Float16*)out, (_Float16*)lse, rows, nsplit);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -280,7 +280,7 @@ def _decode_split(q_i8, sq, kv, O, lse, B, Hq, Sq, qks, st):
                   bhv, rows, Sk, 1, 0, D, qks, st)
         return
     nsplit = -(-Sk // ks)
-    opart = torch.empty((nsplit, bhv * rows, D), dtype=torch.float32, device=O.device)
+    opart = torch.empty((nsplit, bhv * rows, D), dtype=torch.float16, device=O.device)
     ml = torch.empty((nsplit, bhv * rows, 2), dtype=torch.float32, device=O.device)
     _lib.call("qattn_int8_attn_fwd_split", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
               _lib.ptr(kv.sk), _lib.ptr(kv.vt()), _lib.ptr(kv.sv), _lib.ptr(opart), _lib.ptr(ml),
