@@ -1,7 +1,8 @@
 // Forward-mode tangent attention for gfx950; replaces helion_attention_jvp_forward_fp32
 // (attention_jvp.py:24-195).  With P = softmax(q k^T * sm) and tS = (tq k^T + q tk^T) * sm:
 //   H = P o tS,   tO = (P tV + H V - rowsum(H) * O) / l     (jvp:148-190, Appendix A.3)
-// computed online over key tiles with the usual running-max rescale applied to every accumulator.
+// computed online over key tiles with the running-max rescale applied to every accumulator (deferred
+// until the max grows by more than JVP_THR).
 // A = P tV and B = H V only ever appear as A + B, so one accumulator (AB) holds both:
 //   AB^T[d][q] += tV^T P^T + V^T H^T    (two MFMA chains into the same registers).
 // Per 32-key tile and wave: S^T (8), tS^T (16), O^T (8), AB^T (16) v_mfma_f32_32x32x16_bf16 at
@@ -25,6 +26,9 @@ namespace qattn {
 // forward of AttentionJVP_autograd_function.  Its S, P, l and O arithmetic is the
 // same instruction sequence as the tangent kernel's, so O / lse are bit-identical to the ones
 // qattn_jvp_fwd returns (tests/test_gpu_jvp.py).
+// running-max deferral threshold (log2 units) of the online softmax
+constexpr float JVP_THR = 8.0f;
+
 template <int D, bool X3, bool TAN = true>
 struct JvpCfg {
   static constexpr int KB = X3 ? 32 : 64;     // keys per stage
@@ -96,7 +100,8 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
   const int nq = (Sq + 127) / 128;
   int bh, qt;
   xcd_remap(blockIdx.x, nq, a.BH, bh, qt);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: `active` is a scalar branch
   const int q0 = qt * 128 + wave * 32;
   const bool active = q0 < Sq;
   const int qi = q0 + c32;
@@ -174,11 +179,30 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) rl = fmaxf(rl, sacc[i]);
         const float rmax = fmaxf(rl, xor32_f(rl));
-        const float nm = fmaxf(m, rmax * qks);   // jvp:155-158
+        // Deferred running max (cdna_hip_programming.md T13; as int8_attn_fwd): the reference moves m
+        // to max(m, rowmax) on every tile (jvp:155-158, 164) and rescales l, r, O, A, B by
+        // exp2(m - nm).  Here m moves only when some row's tile max exceeds it by more than JVP_THR
+        // (log2 units): P = exp2(S qks - m) <= 2^JVP_THR stays in range, and l, r, O, A + B share
+        // the same (possibly stale) reference, so O = O/l, tO and lse = m + log2 l are unchanged up
+        // to rounding -- while the rescale of the 128 accumulator registers, taken on most tiles of
+        // a 32-row wave with the exact rule, becomes rare.
+        const float cand = fmaxf(m, rmax * qks);
+        if (__ballot(cand > m + JVP_THR)) {
+          asm volatile("" ::: "memory");   // keep the rare rescale a branch
+          const float rs = exp2_f32(m - cand);
+          m = cand;
+          l *= rs;
+          if constexpr (TAN) racc *= rs;
+#pragma unroll
+          for (int b = 0; b < C::NDB; ++b) {
+            o[b] *= rs;
+            if constexpr (TAN) ab[b] *= rs;
+          }
+        }
         float p[16], hh[16], lt = 0.f, rt = 0.f;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          p[i] = exp2_f32(sacc[i] * qks - nm);     // jvp:160-161
+          p[i] = exp2_f32(sacc[i] * qks - m);      // jvp:160-161
           lt += p[i];
           if constexpr (TAN) {
             hh[i] = p[i] * (tacc[i] * sm);         // jvp:152-153,176
@@ -187,17 +211,8 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
         }
         lt += xor32_f(lt);
         if constexpr (TAN) rt += xor32_f(rt);
-        const float rs = exp2_f32(m - nm);         // jvp:164
-        l = l * rs + lt;
-        if constexpr (TAN) racc = racc * rs + rt;  // jvp:178
-        m = nm;
-        if (__ballot(rs != 1.0f)) {
-#pragma unroll
-          for (int b = 0; b < C::NDB; ++b) {
-            o[b] *= rs;
-            if constexpr (TAN) ab[b] *= rs;
-          }
-        }
+        l += lt;
+        if constexpr (TAN) racc += rt;             // jvp:178
         v8bf pb[2][NI], hb[2][NI];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -237,6 +252,8 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
             }
           }
         }
+
+
       }
     }
     dma_wait_barrier();
