@@ -34,6 +34,11 @@ CFLAGS = [
 FILE_FLAGS = {
     "bf16_fwd.hip": ["-fno-slp-vectorize", "-mno-amdgpu-ieee", "-fno-honor-nans"],
     "bf16_bwd.hip": ["-fno-slp-vectorize"],
+    # The JVP forward (one wave per SIMD, 4 fp32 accumulator sets) needs more than 256 registers:
+    # by default hipcc gives the MFMAs AGPR accumulators and copies all 128 of them to VGPRs at every
+    # loop iteration for the (rare) rescale; the VGPR form keeps them in VGPRs and moves the Q
+    # fragments to AGPRs instead (287 instead of 534 vector instructions per 64 keys).
+    "jvp_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
 }
 
 
