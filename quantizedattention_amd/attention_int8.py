@@ -150,18 +150,25 @@ def _ws_chunk(chunk, causal, bkv, sk):
 
 
 def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=None, causal=False,
-                   kv_heads=None, use_ws=None, ws_chunk=None):
+                   kv_heads=None, use_ws=None, ws_chunk=None, kv_len=None):
     """Corrected int8 backward; q_bf / k_bf: bf16 images from the forward (computed here if None).
 
     kv_heads: key/value heads (default: those of O); their token count follows from k_i8T.
     use_ws: dQ from the dS workspace (True), by recomputation (False), or by size (None).
-    ws_chunk: key/value heads per workspace chunk (None: WS_CHUNK / auto; 0 = all heads at once)."""
+    ws_chunk: key/value heads per workspace chunk (None: WS_CHUNK / auto; 0 = all heads at once).
+    kv_len: key/value tokens, needed only to shape the (empty) gradients of an empty batch."""
     O = O.to(torch.float16).contiguous()
     dO = dO.to(torch.float16).contiguous()
     _lib.require_gpu(dO, O, q_i8)
     B, H, S, D = O.shape
     Hkv = H if kv_heads is None else int(kv_heads)
     Nkv = k_i8T.shape[1]
+    if B * H * S == 0 or Nkv == 0:
+        # nothing attends: zero gradients (an empty batch gives empty ones)
+        Sk = Nkv // (B * Hkv) if B * Hkv else int(kv_len if kv_len is not None else S)
+        z = dict(dtype=torch.float16, device=O.device)
+        return (torch.zeros((B, H, S, D), **z), torch.zeros((B, Hkv, Sk, D), **z),
+                torch.zeros((B, Hkv, Sk, D), **z))
     if H % Hkv != 0 or Nkv % (B * Hkv) != 0:
         raise _lib.QAttnError("qattn int8 backward: inconsistent key/value heads")
     Sk = Nkv // (B * Hkv)
@@ -308,7 +315,7 @@ class SageAttention3_Int8_autograd_function(Function):
         ctx.save_for_backward(O, lse, k_mean, q_i8, k_i8T, v_i8, sq, sk, sv)  # int8:58-64
         ctx.args = (Bq, Bkv)
         ctx.images = _take_images(q_i8)
-        ctx.opts = (causal, k_fp16.shape[1], len(inputs) - 3)
+        ctx.opts = (causal, k_fp16.shape[1], len(inputs) - 3, k_fp16.shape[2])
 
     @staticmethod
     def backward(ctx, dO_fp16, _lse, _k_mean, _q_i8, _k_i8T, _v_i8, _sq, _sk, _sv, _Bq, _Bkv):
@@ -319,11 +326,11 @@ class SageAttention3_Int8_autograd_function(Function):
             raise _lib.QAttnError("qattn int8 backward is built for Bq = Bkv = 32")
         q_bf, k_bf = ctx.images   # (None, None): the backward rebuilds them from q_i8 / k_i8
         ctx.images = None
-        causal, kv_heads, nopts = ctx.opts
+        causal, kv_heads, nopts, kv_len = ctx.opts
         with torch._C._DisableFuncTorch():
             dO_fp16 = torch.zeros_like(O) if dO_fp16 is None else _lib.plain(dO_fp16)
             dq, dk, dv = _int8_backward(dO_fp16, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf, k_bf,
-                                        causal=causal, kv_heads=kv_heads)
+                                        causal=causal, kv_heads=kv_heads, kv_len=kv_len)
         return (dq, dk, dv) + (None,) * nopts
 
 

@@ -278,6 +278,9 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   _Float16 mt = (_Float16)(-INFINITY);   // CAUSAL: the reference's (undeferred) running max
   float l = 0.f;      // per-lane partial (this lane's key half); the reference's l = 1 is wiped by r = 0
   float obias = 0.f;  // PV_I8: sum of the tile dequantisation factors (the KMAG bias of O is KMAG * obias)
+  // PV_I8: the dequantisation factor of the tile whose P.V is in flight while SM1 of the next tile
+  // runs; a running-max move there rescales it with O (its int32 product is added after SM1)
+  float cpv_pend = 0.f;
 
   auto slot_of = [&](int t) -> const char* { return smem + (t & (C::NSLOT - 1)) * C::SLOT; };
 
@@ -375,7 +378,10 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       const float r = exp2_f32((float)(_Float16)(m - nm));
       m = nm;
       l *= r;
-      if constexpr (PV == PV_I8) obias *= r;
+      if constexpr (PV == PV_I8) {
+        obias *= r;
+        cpv_pend *= r;
+      }
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b) o[b] *= r;
     }
@@ -503,10 +509,10 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       __builtin_amdgcn_sched_barrier(0);
       v4u pw[2];
       sm2(st, e, pw);
-      const float cpv = st.cpv;
+      cpv_pend = st.cpv;
       pv_mma(va, pw);
-      sm1(nacc, tn, st);
-      pv_dequant(cpv);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
+      sm1(nacc, tn, st);   // (may rescale O, obias and cpv_pend)
+      pv_dequant(cpv_pend);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
     }
   }
   vmcnt_wait_all();
@@ -647,7 +653,7 @@ extern "C" int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, con
                                            const void* sk, const void* vt, const void* sv, void* out,
                                            void* lse, long bh, long sq_tok, long sk_tok, int group,
                                            int causal, int head_dim, float qks, void* stream) {
-  if (sv == nullptr) return 1;
+  if (sv == nullptr && bh > 0 && sq_tok > 0) return 1;   // (empty problems: nothing to read)
   return fwd_dispatch<PV_I8>(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, causal,
                              head_dim, qks, stream);
 }

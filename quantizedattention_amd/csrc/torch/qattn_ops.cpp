@@ -93,6 +93,7 @@ std::tuple<Tensor, Tensor> int8_quant(const Tensor& x, int64_t block) {
   std::vector<int64_t> ss(xh.sizes().begin(), xh.sizes().end() - 2);
   ss.push_back(S / 32);
   Tensor scale = empty(ss, at::kHalf, xh);
+  if (rows == 0) return {idx, scale};
   call(qattn_int8_quant(P(xh), P(idx), P(scale), nullptr, nullptr, rows, (int)S, (int)D, c.stream),
        "int8_quant");
   return {idx, scale};
@@ -129,6 +130,11 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
   Tensor vop = empty({Nkv, D}, f16pv ? at::kHalf : at::kChar, q);
   Tensor O = empty({B, H, S, D}, at::kHalf, q), lse = empty({N}, at::kHalf, q);
   Tensor k_mean;
+  if (N == 0 || Nkv == 0) {   // an empty problem: nothing to read, zero outputs
+    O.zero_();
+    lse.zero_();
+    return {O, lse, q_i8, k_i8, v_i8, sq, sk, sv};
+  }
   if (smooth) {
     k_mean = empty({B, Hkv, 1, D}, at::kHalf, q);
     call(qattn_kmean(P(k), P(k_mean), B * Hkv, Sk, (int)D, c.stream), "kmean");
@@ -165,6 +171,12 @@ T3 int8_bwd(const Tensor& dO_in, const Tensor& q_i8_in, const Tensor& sq, const 
   const Tensor O = O_in.to(at::kHalf).contiguous(), dO = dO_in.to(at::kHalf).contiguous();
   const int64_t B = O.size(0), H = O.size(1), S = O.size(2), D = O.size(3), Hkv = kv_heads;
   const int64_t Nkv = k_i8_in.size(0);
+  if (B * H * S == 0 || Nkv == 0) {   // nothing attends: zero gradients
+    TORCH_CHECK(Hkv > 0, "qattn int8 backward: inconsistent key/value heads");
+    const int64_t Sk0 = B * Hkv ? Nkv / (B * Hkv) : 0;
+    auto z = O_in.options().dtype(at::kHalf);
+    return {at::zeros({B, H, S, D}, z), at::zeros({B, Hkv, Sk0, D}, z), at::zeros({B, Hkv, Sk0, D}, z)};
+  }
   TORCH_CHECK(Hkv > 0 && H % Hkv == 0 && Nkv % (B * Hkv) == 0,
               "qattn int8 backward: inconsistent key/value heads");
   const int64_t Sk = Nkv / (B * Hkv), N = B * H * S, G = H / Hkv;
@@ -233,6 +245,7 @@ std::tuple<Tensor, Tensor> bf16_fwd(const Tensor& q_in, const Tensor& k_in, cons
                v = v_in.to(at::kBFloat16).contiguous();
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3), Sk = k.size(2);
   Tensor O = empty({B, H, S, D}, at::kFloat, q), lse = empty({B * H, S}, at::kFloat, q);
+  if (O.numel() == 0 || k.numel() == 0) return {O.zero_(), lse.zero_()};
   call(qattn_bf16_fwd_ex(P(q), P(k), P(v), P(O), P(lse), B * H, S, Sk, (int)(H / k.size(1)),
                          causal ? 1 : 0, (int)D, qk_scale(D), c.stream),
        "bf16 forward");
@@ -250,6 +263,10 @@ T3 bf16_bwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, const Te
                dO = dO_in.to(at::kFloat).contiguous(), lse = lse_in.to(at::kFloat).contiguous();
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
   const int64_t Hkv = k.size(1), Sk = k.size(2);
+  if (q.numel() == 0 || k.numel() == 0) {   // nothing attends: zero gradients
+    auto z = q.options().dtype(at::kFloat);
+    return {at::zeros(q.sizes(), z), at::zeros(k.sizes(), z), at::zeros(v.sizes(), z)};
+  }
   Tensor dO_bf = empty({B, H, S, D}, at::kBFloat16, q), LD = empty({B * H, S, 2}, at::kFloat, q);
   call(qattn_bf16_bwd_prep(P(dO), P(O), P(lse), P(dO_bf), P(LD), B * H, S, (int)D, c.stream),
        "bf16 backward prep");
@@ -298,6 +315,7 @@ T3 jvp_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& tq, 
   Ctx c(q);
   Tensor O = empty({B, H, S, D}, at::kFloat, q), tO = empty({B, H, S, D}, at::kFloat, q),
          lse = empty({B * H, S}, at::kFloat, q);
+  if (O.numel() == 0 || k.numel() == 0) return {O.zero_(), tO.zero_(), lse.zero_()};
   const float qks = qk_scale(D), sm = sm_scale(D);
   const int G = (int)(H / Hkv);
   const Tensor* ins[6] = {&q, &k, &v, &tq, &tk, &tv};
@@ -342,6 +360,7 @@ Tensor mxfp4_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in) {
                v = v_in.to(at::kHalf).contiguous();
   const int64_t B = q.size(0), H = q.size(1), Sq = q.size(2), D = q.size(3), Hkv = k.size(1),
                 Sk = k.size(2);
+  if (q.numel() == 0 || k.numel() == 0) return at::zeros({B, H, Sq, D}, q.options());
   Tensor k_mean = empty({B, Hkv, 1, D}, at::kHalf, q);
   call(qattn_kmean(P(k), P(k_mean), B * Hkv, Sk, (int)D, c.stream), "kmean");
   Tensor q4 = empty({B * H * Sq, D / 2}, at::kByte, q), qs = empty({B * H * Sq, D / 32}, at::kByte, q);

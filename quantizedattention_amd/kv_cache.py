@@ -273,6 +273,8 @@ def _decode_split(q_i8, sq, kv, O, lse, B, Hq, Sq, qks, st):
       and merged (qattn_int8_split_combine), so that the grid fills the chip."""
     _, Hkv, Sk, D = kv.shape
     bhv, rows = B * Hkv, (Hq // Hkv) * Sq
+    if bhv * rows == 0:
+        return
     ks = _split_plan(bhv, rows, Sk)
     if ks >= Sk:
         _lib.call("qattn_int8_attn_fwd_i8pv_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),

@@ -93,6 +93,7 @@ def _int8_setup(ctx, inputs, output):
     ctx.save_for_backward(O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
     ctx.causal, ctx.kv_heads = causal, k.shape[1]
     ctx.dtypes = (q.dtype, k.dtype, v.dtype)
+    ctx.kv_shape = k.shape
 
 
 def _int8_backward_rule(ctx, dO, *_unused):
@@ -101,9 +102,13 @@ def _int8_backward_rule(ctx, dO, *_unused):
     O, lse, q_i8, k_i8, v_i8, sq, sk, sv = ctx.saved_tensors
     if dO is None:
         return None, None, None, None, None
+    qd, kd, vd = ctx.dtypes
+    if O.numel() == 0 or k_i8.numel() == 0:   # nothing attends (an empty batch): zero gradients
+        z = dict(device=O.device)
+        return (torch.zeros(O.shape, dtype=qd, **z), torch.zeros(ctx.kv_shape, dtype=kd, **z),
+                torch.zeros(ctx.kv_shape, dtype=vd, **z), None, None)
     dq, dk, dv = _ops.int8_bwd(dO.to(torch.float16), q_i8, sq, k_i8, sk, v_i8, sv, O, lse, ctx.causal,
                                ctx.kv_heads)
-    qd, kd, vd = ctx.dtypes
     return dq.to(qd), dk.to(kd), dv.to(vd), None, None
 
 
