@@ -29,6 +29,13 @@ int qattn_probe_mfma_fp4(const void* A, const void* B, const void* sa, const voi
                          void* stream);
 int qattn_probe_fp4_cvt(const void* x, const void* s, void* packed, void* back, void* stream);
 
+/* The int8 quantiser's division-free index (common.h quant8) vs the IEEE fp32 division, over every
+ * finite fp16 x with |x| < 127.5 s (a block holds |x / s| <= 127.07) and the fp16 scales s with
+ * bit patterns in [s_lo, s_hi); bad[0]
+ * (unsigned[6], zeroed by the caller) counts mismatching indices / images, bad[1..5] = the first
+ * (s bits, x bits, reference index, index, image bits). */
+int qattn_probe_quant_div(int s_lo, int s_hi, void* bad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

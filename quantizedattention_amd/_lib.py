@@ -86,6 +86,7 @@ DEV_SIGNATURES = {
     "qattn_probe_mfma_fp4": [_vp] * 6,
     "qattn_probe_fp4_cvt": [_vp] * 5,
     "qattn_probe_fwd_helpers": [_vp] * 7,
+    "qattn_probe_quant_div": [_c_int, _c_int, _vp, _vp],
 }
 
 # return types other than the int status code

@@ -129,6 +129,44 @@ QA_DEVICE float pair_max(float x) {
 QA_DEVICE void exp2_pk4(const v2h* x, v2h* r) { QA_PK4("v_exp_f16"); }
 QA_DEVICE void trunc_pk4(const v2h* x, v2h* r) { QA_PK4("v_trunc_f16"); }
 
+// ---------------------------------------------------------------- int8 block quantiser
+// idx = trunc(RNE_f16(fp32(x) / s)) (int8:178-186: IEEE fp32 division, fp16 rounding, trunc) for
+// fp16 x and the block scale s = f16(amax / 127), without a division per element: r = v_rcp_f32(s)
+// (1 ulp), q0 = x r and one Newton step q1 = q0 + (x - q0 s) r, so |q1 - x/s| <= 0.5 ulp + 2^-44
+// |x/s|.  x / s is never an fp16 rounding midpoint and lies at least one fp32 ulp away from every
+// midpoint (a midpoint's odd 12-bit significand times the significand of s has more than the 11
+// bits of x), so RNE_f16(q1) = RNE_f16(x / s) bit for bit -- checked exhaustively over every fp16
+// x and s (qattn_probe_quant_div, tests/test_gpu_layout.py).  r = 0 for s = 0 gives q1 = 0 (the
+// reference's idx 0 for an all-zero block).
+QA_DEVICE float quant_rcp(float s) { return s != 0.f ? __builtin_amdgcn_rcpf(s) : 0.f; }
+QA_DEVICE float quant_div(float x, float s, float r) {
+  const float q0 = x * r;
+  return __builtin_fmaf(__builtin_fmaf(-q0, s, x), r, q0);
+}
+// 8 fp16 values of a block -> their int8 indices (lo: values 0..3, hi: 4..7, byte j = index j)
+// and the indices as exact floats (for the bf16 / f16 images).  trunc on packed halves, then
+// y = t + 1536 (exact: the fp16 spacing is 1 in [1024, 2048)) holds t in its low byte and gives
+// t = y - 1536 as a float without a -0.
+QA_DEVICE void quant8(const v8h& x, float s, float r, unsigned& lo, unsigned& hi, float* qf) {
+  v2h h[4], t[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    h[k] = __builtin_bit_cast(v2h, pk_f16(quant_div((float)x[2 * k], s, r),
+                                          quant_div((float)x[2 * k + 1], s, r)));
+  trunc_pk4(h, t);
+  const v2h k1536 = {(_Float16)1536.0f, (_Float16)1536.0f};
+  unsigned u[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const v2h y = t[k] + k1536;
+    u[k] = __builtin_bit_cast(unsigned, y);
+    qf[2 * k] = (float)y[0] - 1536.0f;
+    qf[2 * k + 1] = (float)y[1] - 1536.0f;
+  }
+  lo = __builtin_amdgcn_perm(u[1], u[0], 0x06040200u);
+  hi = __builtin_amdgcn_perm(u[3], u[2], 0x06040200u);
+}
+
 // d[j] = {f16(a[2j]*c + n), f16(a[2j+1]*c + n)}, one rounding each (v_fma_mix, f32 sources).  All 8
 // low halves are written before the high halves so that no mixhi reads a just-written VGPR.
 QA_DEVICE void fma_mix8(const float* a, float c, float n, v2h* d) {

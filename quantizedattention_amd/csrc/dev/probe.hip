@@ -157,3 +157,50 @@ extern "C" int qattn_probe_fp4_cvt(const void* x, const void* s, void* packed, v
                      (const float*)s, (unsigned*)packed, (float*)back);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// The int8 quantiser's division-free index (common.h quant8) against the IEEE fp32 division of the
+// reference, trunc(RNE_f16(fp32(x) / s)), for every finite fp16 x with |x| < 127.5 s (the range a
+// block with scale s = f16(amax / 127) can hold; other x are replaced by 0) and every fp16 scale
+// s in [s_lo, s_hi) (bit patterns).  Thread: 8 consecutive x bit patterns; grid.y strides over s.
+// Mismatching bytes or image values are counted in bad[0] (vector atomics, only on a mismatch);
+// bad[1..5] hold the first one found.
+namespace qattn {
+__global__ __launch_bounds__(256) void probe_quant_div_kernel(int s_lo, int s_hi, unsigned* bad) {
+  const unsigned x0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  for (int sb = s_lo + (int)blockIdx.y; sb < s_hi; sb += (int)gridDim.y) {
+    const float s = (float)__builtin_bit_cast(_Float16, (unsigned short)sb);
+    v8h x;
+    int ref[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      _Float16 xv = __builtin_bit_cast(_Float16, (unsigned short)(x0 + j));
+      const float xf = (float)xv;
+      if (!(fabsf(xf) < 127.5f * s)) xv = (_Float16)0.0f;   // (also NaN / inf)
+      x[j] = xv;
+      ref[j] = s != 0.f ? (int)__builtin_truncf((float)(_Float16)((float)xv / s)) : 0;
+    }
+    unsigned lo, hi;
+    float qf[8];
+    quant8(x, s, quant_rcp(s), lo, hi, qf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int byte = (int)(signed char)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 0xff);
+      if ((byte != ref[j]) || (__float_as_uint(qf[j]) != __float_as_uint((float)ref[j]))) {
+        // bad[0]: count; bad[1..5]: the first mismatch (s bits, x bits, reference, byte, image bits)
+        if (atomicAdd(bad, 1u) == 0) {
+          bad[1] = (unsigned)sb;
+          bad[2] = (unsigned)__builtin_bit_cast(unsigned short, x[j]);
+          bad[3] = (unsigned)ref[j];
+          bad[4] = (unsigned)byte;
+          bad[5] = __float_as_uint(qf[j]);
+        }
+      }
+    }
+  }
+}
+}  // namespace qattn
+extern "C" int qattn_probe_quant_div(int s_lo, int s_hi, void* bad, void* stream) {
+  hipLaunchKernelGGL(probe_quant_div_kernel, dim3(65536 / 8 / 256, 1024), dim3(256), 0, (hipStream_t)stream,
+                     s_lo, s_hi, (unsigned*)bad);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -100,20 +100,14 @@ __global__ __launch_bounds__(256) void int8_bwd_prep_kernel(
   amax = wave_max_f(amax);
   const _Float16 s16 = (_Float16)(amax / 127.0f);
   const float s = (float)s16;
+  const float r = quant_rcp(s);
   if (lane == 0) scale[blk] = s16;
 #pragma unroll
   for (int i = 0; i < ITERS; ++i) {
     const int e = (i * 64 + lane) * 8;
-    unsigned lo = 0, hi = 0;
+    unsigned lo, hi;
     float qf[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      int qi = 0;
-      if (s != 0.f) qi = (int)__builtin_truncf((float)(_Float16)((float)v[i][j] / s));
-      const unsigned b = (unsigned)(qi & 0xff);
-      if (j < 4) lo |= b << (8 * j); else hi |= b << (8 * (j - 4));
-      qf[j] = (float)qi;
-    }
+    quant8(v[i], s, r, lo, hi, qf);   // (common.h: the reference's division, exactly)
     *reinterpret_cast<v2u*>(idx + blk * ELEMS + e) = v2u{lo, hi};
     if constexpr (IMG) {
       const v4u w = {pk_bf16(qf[0], qf[1]), pk_bf16(qf[2], qf[3]), pk_bf16(qf[4], qf[5]),

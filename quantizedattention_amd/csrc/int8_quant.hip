@@ -3,8 +3,10 @@
 // (build contract for attention_int8.py:24-25).
 //
 // Numerics (bit-exact with the eager reference):
-//   s   = RNE_fp16( fp32(amax|X|) / 127 )            (IEEE fp32 divide)
-//   idx = trunc( RNE_fp16( fp32(x) / fp32(s) ) )      (IEEE fp32 divide, fp16 round, then trunc)
+//   s   = RNE_fp16( fp32(amax|X|) / 127 )            (IEEE fp32 divide, once per block)
+//   idx = trunc( RNE_fp16( fp32(x) / fp32(s) ) )      (fp16 round, then trunc; the division as a
+//                                                       reciprocal and one Newton step, exactly:
+//                                                       common.h quant_div)
 // An all-zero block (s == 0) yields idx 0.
 //
 // HBM-bound: one wave per 32-token block (32 x D fp16 = 8 KB for D=128), 16-byte loads/stores,
@@ -47,21 +49,18 @@ __global__ __launch_bounds__(256) void quant_block32_kernel(
   amax = wave_max_f(amax);
   const _Float16 s16 = (_Float16)(amax / 127.0f);
   const float s = (float)s16;
+  const float r = quant_rcp(s);
   if (lane == 0) scale[blk] = s16;
 #pragma unroll
   for (int i = 0; i < ITERS; ++i) {
     const int e = (i * 64 + lane) * 8;
-    unsigned lo = 0, hi = 0;
+    unsigned lo, hi;
     v8h dq;
     float qf[8];
+    quant8(v[i], s, r, lo, hi, qf);
+    if constexpr (DEQ) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      int qi = 0;
-      if (s != 0.f) qi = (int)__builtin_truncf((float)(_Float16)((float)v[i][j] / s));
-      const unsigned b = (unsigned)(qi & 0xff);
-      if (j < 4) lo |= b << (8 * j); else hi |= b << (8 * (j - 4));
-      if constexpr (DEQ) dq[j] = (_Float16)((float)qi * s);
-      qf[j] = (float)qi;
+      for (int j = 0; j < 8; ++j) dq[j] = (_Float16)(qf[j] * s);
     }
     *reinterpret_cast<v2u*>(idx + blk * ELEMS + e) = v2u{lo, hi};
     if constexpr (DEQ) *reinterpret_cast<v8h*>(deq + blk * ELEMS + e) = dq;
@@ -81,14 +80,6 @@ __global__ __launch_bounds__(256) void quant_block32_kernel(
 // -- the A operand of v_mfma_i32_32x32x32_i8 for V^T in the key order of the S^T accumulator
 // (common.h).  Lane (row c, half h) loads v[c][32b + 16h .. +16]: exactly the A operand of the
 // block in natural order, which one i8 MFMA against the identity transposes into that image.
-QA_DEVICE v4i pack16_i8(const int* q) {
-  v4i a;
-#pragma unroll
-  for (int w = 0; w < 4; ++w)
-    a[w] = (q[4 * w] & 0xff) | ((q[4 * w + 1] & 0xff) << 8) | ((q[4 * w + 2] & 0xff) << 16) |
-           (q[4 * w + 3] << 24);
-  return a;
-}
 template <int D>
 __global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restrict__ v,
                                                        int8_t* __restrict__ vi,
@@ -112,15 +103,16 @@ __global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restric
   amax = wave_max_f(amax);
   const _Float16 s16 = (_Float16)(amax / 127.0f);
   const float s = (float)s16;
+  const float r = quant_rcp(s);
   if (lane == 0) sv[blk] = s16;
   const v4i ident = identity_b_i8(lane);
 #pragma unroll
   for (int b = 0; b < NDB; ++b) {
-    int q[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      q[j] = s != 0.f ? (int)__builtin_truncf((float)(_Float16)((float)x[b][j >> 3][j & 7] / s)) : 0;
-    const v4i a = pack16_i8(q);
+    unsigned w[4];
+    float qf[8];
+    quant8(x[b][0], s, r, w[0], w[1], qf);
+    quant8(x[b][1], s, r, w[2], w[3], qf);
+    const v4i a = {(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
     *reinterpret_cast<v4i*>(vi + row * D + 32 * b + 16 * h) = a;
     const v16i t = mfma_i8(a, ident, v16i{});
     *reinterpret_cast<v4i*>(vt + blk * 32 * D + b * 1024 + 16 * lane) = pack_acc_bytes(t);

@@ -79,3 +79,19 @@ def test_int8_fwd_softmax_helpers(lib):
     assert torch.equal(w.cpu().view(torch.int16), exp_w.view(torch.int16))
     exp_d = (a.double() * cn[lane, 0].double() + cn[lane, 1].double()).half()
     assert torch.equal(d.cpu().view(torch.int16), exp_d.view(torch.int16))
+
+
+def test_quant_div_exhaustive(lib):
+    """The quantisers' division-free index (common.h quant8: reciprocal + one Newton step) equals
+    trunc(f16(fp32(x) / s)) with the IEEE fp32 division for every finite fp16 x with |x| < 127.5 s
+    (a block holds |x / s| <= 127.07) and
+    every fp16 scale s >= 0 (bit patterns 0 .. 0x7BFF; s = 0 gives idx 0)."""
+    from quantizedattention_amd import _lib
+    bad = torch.zeros((8,), dtype=torch.int32, device="cuda")
+    st = _lib.stream_of(bad)
+    for lo in range(0, 0x7C00, 0x2000):
+        _lib.call("qattn_probe_quant_div", lo, min(lo + 0x2000, 0x7C00), _lib.ptr(bad), st)
+    torch.cuda.synchronize()
+    b = bad.cpu().tolist()
+    assert b[0] == 0, (f"{b[0]} mismatches; first: s=0x{b[1]:04x} x=0x{b[2]:04x} ref={b[3]} "
+                       f"byte={b[4]} image=0x{b[5] & 0xffffffff:08x}")

@@ -1,0 +1,47 @@
+"""Kernels of one int8 fwd+bwd step at config 3 in launch order, with durations and the idle gaps
+between them (dev tool; run under rocprofv3 --kernel-trace --output-format csv, then
+python tools/step_trace.py --report <kernel_trace.csv>)."""
+import csv
+import os
+import sys
+
+
+def run():
+    import torch
+    sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
+    from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward
+    g = torch.Generator(device="cuda").manual_seed(0)
+    B, H, S, D = 4, 32, 4096, 128
+    q, k, v = (torch.randn((B, H, S, D), device="cuda", generator=g).half() for _ in range(3))
+    dO = (torch.randn((B, H, S, D), device="cuda", generator=g) * 1e-3).half()
+
+    def step():
+        O, lse, qi, kiT, vi, sq, sk, sv, km, qb_, kb_ = _int8_forward(q, k, v, smooth=True, images=True)
+        _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb_, kb_)
+    for _ in range(6):
+        step()
+    torch.cuda.synchronize()
+    print("done", flush=True)
+
+
+def report(path):
+    rows = list(csv.DictReader(open(path)))
+    ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
+    # the last step: from the last k-mean launch on
+    first = max(i for i, k in enumerate(ks) if "kmean" in k[2])
+    prev = None
+    tot_k = 0.0
+    for s, e, n in ks[first:]:
+        gap = (s - prev) / 1e3 if prev else 0.0
+        tot_k += (e - s) / 1e3
+        print(f"{(e - s) / 1e3:9.1f} us  gap {gap:7.1f}  {n[:110]}")
+        prev = e
+    span = (ks[-1][1] - ks[first][0]) / 1e3
+    print(f"step span {span:.1f} us, kernel time {tot_k:.1f} us, idle {span - tot_k:.1f} us")
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--report":
+        report(sys.argv[2])
+    else:
+        run()
