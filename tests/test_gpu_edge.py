@@ -146,3 +146,85 @@ def test_running_max_moves_vs_oracle(lib, monkeypatch, D, causal, pv):
         # 1.3e-2 .. 1.8e-2 from the reference with both 0.03 .. 0.89 from exact attention.
         assert d_ref <= 3e-2
         assert e_ours <= e_ref + 1e-2
+
+
+def _ramp_inputs(shape, seed, kscale=24.0):
+    """q random, k scaled by a ramp along the keys (the row max climbs tile after tile), v random."""
+    B, H, S, D = shape
+    g = torch.Generator().manual_seed(seed)
+    ramp = (1.0 + torch.arange(S, dtype=torch.float32) / kscale).view(1, 1, S, 1)
+    q = torch.randn(shape, generator=g)
+    k = torch.randn(shape, generator=g) * ramp
+    v = torch.randn(shape, generator=g)
+    return q, k, v
+
+
+def test_bf16_running_max_moves_vs_oracle(lib):
+    """The bf16 forward (exact running-max rule, rescale on every move, the reference's beta rule)
+    on a climbing row max, causal.  The beta rule compares raw scores with the scaled max
+    (bf16:248) and doubles m when two raw scores pass it; on these inputs it fires on most late
+    tiles, and whether it fires hinges on single bf16 steps of S (ties M2 == thr on the bf16 grid),
+    which the fp32 accumulation order of the S product can move -- the oracle's CPU matmul and the
+    MFMA sum in different orders, as the reference's own GPU kernel would.  A flipped decision
+    changes m by 2x from then on (and can push every P of the row below the fp32 denormal range,
+    which v_exp_f32 flushes: l = 0).  Bar: >= 95 % of the rows within 5e-3 of the oracle (measured:
+    501 of 512); non-causal, the doublings overflow m and the oracle itself turns NaN."""
+    from oracle import restate as R
+    from quantizedattention_amd.attention_bf16 import helion_atten_bf16_fwd_training
+    q, k, v = _ramp_inputs((1, 2, 256, 128), 45, kscale=96.0)
+    q, k, v = q.half(), k.half(), v.bfloat16()
+    O_ref, lse_ref = R.bf16_fwd(q, k, v, True, kt=16)
+    assert torch.isfinite(O_ref).all()
+    O, lse = helion_atten_bf16_fwd_training(q.cuda(), k.cuda(), v.cuda(), True)
+    D = O.shape[-1]
+    e_O = (O.cpu().view(-1, D) - O_ref.view(-1, D)).abs().max(-1).values
+    e_l = (lse.cpu().view(-1) - lse_ref.view(-1)).abs()
+    ok = (e_O <= 5e-3) & (e_l <= 5e-3)    # (NaN compares False)
+    print(f"rows {ok.numel()}, matching the oracle {int(ok.sum())}")
+    assert int(ok.sum()) >= 0.95 * ok.numel()
+
+
+@pytest.mark.parametrize("fp32", [True, False])
+def test_jvp_running_max_moves(lib, fp32):
+    """The JVP forward's deferred running max (moves only past 8 log2 units) on a climbing row max,
+    vs torch.func.jvp of the fp32 baseline.  Bars from the operand precision (these logits reach
+    |S| ~ 45, far past the random inputs of tests/test_gpu_jvp.py): the fp32 mode's products carry
+    the 2^-16 relative residual of the hi/lo split, so O and tO move by up to 2^-16 max|S| max|v|
+    (resp. max|tv| + max|tS| max|v|); the bf16 mode rounds P and H = P tS to bf16 (2^-9), which
+    moves tO by up to 2^-9 max|tS| max|v| (measured 0.33 at max|tO| = 51)."""
+    from oracle import restate as R
+    from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp32
+    q, k, v = _ramp_inputs((1, 2, 256, 128), 46, kscale=16.0)
+    g = torch.Generator().manual_seed(47)
+    tq, tk, tv = (torch.randn(q.shape, generator=g) for _ in range(3))
+    if not fp32:
+        q, k, v, tq, tk, tv = (t.bfloat16().float() for t in (q, k, v, tq, tk, tv))
+    dt = torch.float32 if fp32 else torch.bfloat16
+    O, tO, lse = helion_attention_jvp_forward_fp32(*(t.cuda().to(dt) for t in (q, k, v, tq, tk, tv)))
+    Ot, tOt = R.jvp_truth(q, k, v, tq, tk, tv)
+    sm = q.shape[-1] ** -0.5
+    s_max = (q.abs() @ k.abs().transpose(-1, -2)).max().item() * sm
+    ts_max = ((tq @ k.transpose(-1, -2) + q @ tk.transpose(-1, -2)) * sm).abs().max().item()
+    vm, tvm = v.abs().max().item(), tv.abs().max().item()
+    e_O = (O.cpu() - Ot).abs().max().item()
+    e_tO = (tO.cpu() - tOt).abs().max().item()
+    print(f"fp32={fp32}: |O err| {e_O:.3g}  |tO err| {e_tO:.3g}  max|S| {s_max:.1f}  max|tS| {ts_max:.1f}")
+    if fp32:
+        assert e_O <= 2.0 ** -16 * s_max * vm
+        assert e_tO <= 2.0 ** -16 * s_max * (tvm + ts_max * vm)
+    else:
+        assert e_O <= 1e-2
+        assert e_tO <= 2.0 ** -9 * ts_max * vm
+
+
+def test_mxfp4_running_max_moves_vs_oracle(lib):
+    """The MX-FP4 forward's integer running max (raised past MSLACK) on a climbing row max."""
+    from oracle import mxfp4 as M
+    from quantizedattention_amd.attention_mxfp4 import mxfp4_attn_fwd
+    q, k, v = (t.half() for t in _ramp_inputs((1, 2, 128, 128), 48, kscale=12.0))
+    O, lse, ops = mxfp4_attn_fwd(q.cuda(), k.cuda(), v.cuda(), smooth_k=False)
+    RO, Rl, rops = M.mxfp4_fwd(q, k, v)
+    for a, b in zip(ops, rops):
+        assert torch.equal(a.cpu().reshape(b.shape), b)
+    assert (O.float().cpu() - RO.float()).abs().max().item() <= 2e-2
+    assert (lse.cpu() - Rl).abs().max().item() <= 1e-4 * max(1.0, Rl.abs().max().item())
