@@ -183,7 +183,8 @@ bf16_bwd_kernel(const _Float16* __restrict__ xa, const __bf16* __restrict__ xb,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
   int bh, xt;
-  xcd_remap(blockIdx.x, nxb, BH, bh, xt);
+  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nxb, BH, ROLE == B16_DQ, bh, xt);
+  else xcd_remap(blockIdx.x, nxb, BH, bh, xt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
@@ -386,7 +387,8 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dkv_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
   int bh, xt;
-  xcd_remap(blockIdx.x, nxb, BH, bh, xt);
+  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nxb, BH, false, bh, xt);
+  else xcd_remap(blockIdx.x, nxb, BH, bh, xt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool pwave = wave < 4;
@@ -642,7 +644,8 @@ __global__ __launch_bounds__(512, 2) void bf16_bwd_dqw_kernel(const __bf16* __re
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = (Sq + 32 * W::WAVES - 1) / (32 * W::WAVES);
   int bh, qb;
-  xcd_remap(blockIdx.x, nqb, BH, bh, qb);
+  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nqb, BH, true, bh, qb);
+  else xcd_remap(blockIdx.x, nqb, BH, bh, qb);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;

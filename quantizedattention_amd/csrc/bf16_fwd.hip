@@ -107,7 +107,8 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nq = (Sq + C::QROWS - 1) / C::QROWS;
   int bh, qt;
-  xcd_remap(blockIdx.x, nq, BH, bh, qt);
+  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nq, BH, true, bh, qt);
+  else xcd_remap(blockIdx.x, nq, BH, bh, qt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;

@@ -518,6 +518,24 @@ QA_DEVICE void store_rows(const v16f* acc, float sc, char* lds, T* dst_row0, int
   }
 }
 
+// Causal grids: the work of a workgroup grows with its query block (forward, dQ) or shrinks with
+// its key block (dK/dV).  Dispatch the heaviest block of every head first -- longest-processing-
+// time order, so the light blocks fill the tail -- with every head still on XCD bh & 7.
+// heavy_last: the heaviest block is the last index (query blocks), else the first (key blocks).
+// Speed only, never correctness.
+QA_DEVICE void xcd_remap_lpt(int bid, int nq, int nbh, bool heavy_last, int& bh, int& qt) {
+  int r;
+  if ((nbh & 7) == 0) {
+    const int hpx = nbh >> 3, j = bid >> 3;
+    r = j / hpx;
+    bh = (j % hpx) * 8 + (bid & 7);
+  } else {
+    r = bid / nbh;
+    bh = bid % nbh;
+  }
+  qt = heavy_last ? nq - 1 - r : r;
+}
+
 // Workgroup -> (head, q-tile) remap that keeps every q-tile of one head on one XCD
 // (blocks b and b+8 share an XCD under round-robin dispatch; speed only, never correctness).
 QA_DEVICE void xcd_remap(int bid, int nq, int nbh, int& bh, int& qt) {

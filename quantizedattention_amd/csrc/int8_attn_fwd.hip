@@ -202,7 +202,8 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
 
   const int nq = (Sq + C::QROWS - 1) / C::QROWS;
   int bh, qt;
-  xcd_remap(blockIdx.x, nq, BH, bh, qt);
+  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nq, BH, true, bh, qt);
+  else xcd_remap(blockIdx.x, nq, BH, bh, qt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;

@@ -280,7 +280,8 @@ void int8_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
   int bh, xt;
-  xcd_remap(blockIdx.x, nxb, BH, bh, xt);
+  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nxb, BH, ROLE == ROLE_DQ, bh, xt);
+  else xcd_remap(blockIdx.x, nxb, BH, bh, xt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
@@ -649,7 +650,8 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = (Sq + 32 * W::WAVES - 1) / (32 * W::WAVES);
   int bh, qb;
-  xcd_remap(blockIdx.x, nqb, BH, bh, qb);
+  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nqb, BH, true, bh, qb);
+  else xcd_remap(blockIdx.x, nqb, BH, bh, qb);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;

@@ -1,12 +1,12 @@
 """Kernels of one int8 fwd+bwd step at config 3 in launch order, with durations and the idle gaps
 between them (dev tool; run under rocprofv3 --kernel-trace --output-format csv, then
-python tools/step_trace.py --report <kernel_trace.csv>)."""
+python tools/step_trace.py --report <kernel_trace.csv>); --causal for the causal step."""
 import csv
 import os
 import sys
 
 
-def run():
+def run(causal=False):
     import torch
     sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
     from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward
@@ -16,8 +16,9 @@ def run():
     dO = (torch.randn((B, H, S, D), device="cuda", generator=g) * 1e-3).half()
 
     def step():
-        O, lse, qi, kiT, vi, sq, sk, sv, km, qb_, kb_ = _int8_forward(q, k, v, smooth=True, images=True)
-        _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb_, kb_)
+        O, lse, qi, kiT, vi, sq, sk, sv, km, qb_, kb_ = _int8_forward(q, k, v, smooth=True, images=True,
+                                                                       causal=causal)
+        _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb_, kb_, causal=causal)
     for _ in range(6):
         step()
     torch.cuda.synchronize()
@@ -44,4 +45,4 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--report":
         report(sys.argv[2])
     else:
-        run()
+        run(causal="--causal" in sys.argv)
