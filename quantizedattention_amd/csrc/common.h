@@ -93,6 +93,42 @@ QA_DEVICE float wave_max_dpp(float x) {
   auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return vmax(__uint_as_float(r2[0]), __uint_as_float(r2[1]));
 }
+// Full-wave max of non-negative floats (no -0, no NaN), result in every lane: for such values the
+// float order is the integer order of the bits, and the integer max lets hipcc fold each DPP move
+// into its max (v_max_i32_dpp: one instruction per step, where the float form needs a move and a
+// canonicalising max).  Bit-identical to wave_max_dpp on these inputs.
+QA_DEVICE float wave_max_nonneg(float x) {
+  int v = __float_as_int(x);
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true));   // row_half_mirror
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true));   // row_mirror
+  const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  v = max((int)r[0], (int)r[1]);
+  const auto r2 = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+  return __int_as_float(max((int)r2[0], (int)r2[1]));
+}
+// Two such maxima at once: the steps of the two chains interleave, so each DPP read of a value
+// written one instruction earlier finds the other chain's step in between instead of an s_nop.
+QA_DEVICE void wave_max2_nonneg(float& x, float& y) {
+  int a = __float_as_int(x), b = __float_as_int(y);
+  a = max(a, __builtin_amdgcn_mov_dpp(a, 0xB1, 0xF, 0xF, true));
+  b = max(b, __builtin_amdgcn_mov_dpp(b, 0xB1, 0xF, 0xF, true));
+  a = max(a, __builtin_amdgcn_mov_dpp(a, 0x4E, 0xF, 0xF, true));
+  b = max(b, __builtin_amdgcn_mov_dpp(b, 0x4E, 0xF, 0xF, true));
+  a = max(a, __builtin_amdgcn_mov_dpp(a, 0x141, 0xF, 0xF, true));
+  b = max(b, __builtin_amdgcn_mov_dpp(b, 0x141, 0xF, 0xF, true));
+  a = max(a, __builtin_amdgcn_mov_dpp(a, 0x140, 0xF, 0xF, true));
+  b = max(b, __builtin_amdgcn_mov_dpp(b, 0x140, 0xF, 0xF, true));
+  const auto ra = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)a, false, false);
+  const auto rb = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  a = max((int)ra[0], (int)ra[1]);
+  b = max((int)rb[0], (int)rb[1]);
+  const auto sa = __builtin_amdgcn_permlane32_swap((unsigned)a, (unsigned)a, false, false);
+  const auto sb = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  x = __int_as_float(max((int)sa[0], (int)sa[1]));
+  y = __int_as_float(max((int)sb[0], (int)sb[1]));
+}
 // Value of lane l^32 (half-wave exchange without LDS).  v_permlane32_swap vdst, vsrc swaps
 // vdst[32..63] with vsrc[0..31]: with vdst = vsrc = x, lanes 0-31 find x[l+32] in the new vsrc and
 // lanes 32-63 find x[l-32] in the new vdst.

@@ -408,11 +408,14 @@ void int8_bwd_kernel(
   };
   // per-tile quantisation of X into the two bf16 B operands, scaled by so (the other operand's
   // per-tile scale)
-  auto quantise = [&](const float* X, float so, v8bf* op) {
-    const float xmax = wave_max_dpp(max16_abs3(X));
+  // xmax: the tile's max |X| (wave_max_nonneg of max16_abs3)
+  auto quantise_m = [&](const float* X, float so, v8bf* op, float xmax) {
     const float sx = xmax * (1.0f / 127.0f);
     const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
     quant_operand(X, inv, sx * so, op);
+  };
+  auto quantise = [&](const float* X, float so, v8bf* op) {
+    quantise_m(X, so, op, wave_max_nonneg(max16_abs3(X)));
   };
   auto tr_load = [&](int t, int region, v8bf* ta) {
     const char* base = slot(t) + region;
@@ -446,11 +449,10 @@ void int8_bwd_kernel(
   // dS quantisation (the dK operand, as quantise()) that also emits the workspace record of tile t:
   // the 16 dS_i8 of this lane packed in index order, and s_dS (lane 0).  Two VMEM stores per tile,
   // counted by the ring waits below (WS_OPS).
-  auto quantise_ds = [&](const float* X, int t, v8bf* op) {
+  auto quantise_ds = [&](const float* X, int t, v8bf* op, float xmax) {
     if constexpr (!WS) {
-      quantise(X, so_ds(t), op);
+      quantise_m(X, so_ds(t), op, xmax);
     } else {
-      const float xmax = wave_max_dpp(max16_abs3(X));
       const float sx = xmax * (1.0f / 127.0f);
       const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
       const float c = sx * so_ds(t);
@@ -522,8 +524,10 @@ void int8_bwd_kernel(
       products(t0, sa, pa);
       float P[16], dS[16];
       values(t0, sa, pa, P, dS);
-      quantise_ds(dS, t0, opS);
-      quantise(P, so_p(t0), opP);
+      float mS = max16_abs3(dS), mP = max16_abs3(P);
+      wave_max2_nonneg(mS, mP);   // (the two tile maxima in one interleaved reduction)
+      quantise_ds(dS, t0, opS, mS);
+      quantise_m(P, so_p(t0), opP, mP);
     }
     for (int t = t0; t < nt; ++t) {
       // tile t+1 landed: younger than its DMA are the workspace stores of tile t-1, the DMA of
@@ -543,8 +547,10 @@ void int8_bwd_kernel(
         accumulate(acc2, ta, opP);         // dV += dO^T P
         float P[16], dS[16];
         values(tn, sa, pa, P, dS);
-        quantise_ds(dS, tn, opS);
-        quantise(P, so_p(tn), opP);
+        float mS = max16_abs3(dS), mP = max16_abs3(P);
+        wave_max2_nonneg(mS, mP);   // (the two tile maxima in one interleaved reduction)
+        quantise_ds(dS, tn, opS, mS);
+        quantise_m(P, so_p(tn), opP, mP);
       }
     }
   } else {
@@ -565,8 +571,10 @@ void int8_bwd_kernel(
         float P[16], dS[16];
         values(t, sa, pa, P, dS);
         v8bf opS[2], opP[2];
-        quantise_ds(dS, t, opS);
-        quantise(P, so_p(t), opP);
+        float mS = max16_abs3(dS), mP = max16_abs3(P);
+        wave_max2_nonneg(mS, mP);   // (the two tile maxima in one interleaved reduction)
+        quantise_ds(dS, t, opS, mS);
+        quantise_m(P, so_p(t), opP, mP);
         v8bf ta[2 * C::NDB];
         tr_load(t, G::TR, ta);
         accumulate(acc, ta, opS);          // dK += q^T dS
