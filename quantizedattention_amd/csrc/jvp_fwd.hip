@@ -28,6 +28,14 @@ namespace qattn {
 // qattn_jvp_fwd returns (tests/test_gpu_jvp.py).
 // running-max deferral threshold (log2 units) of the online softmax
 constexpr float JVP_THR = 8.0f;
+// QA_JVP_HLO = 1 (build option, off by default): in the bf16 mode H = P tS also enters the B = H V
+// product as a bf16 lo residual (hi + lo: 16 bits).  The bf16 rounding of H dominates tO's error
+// at large logits: on the climbing-max input of tests/test_gpu_edge.py 0.33 -> 0.053 (max|tO| =
+// 51), for 8 more MFMAs per 32 keys: config 5 0.267 -> 0.30 ms.  The fp32 (X3) mode is the
+// accurate path.
+#ifndef QA_JVP_HLO
+#define QA_JVP_HLO 0
+#endif
 
 template <int D, bool X3, bool TAN = true>
 struct JvpCfg {
@@ -213,16 +221,19 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
         if constexpr (TAN) rt += xor32_f(rt);
         l += lt;
         if constexpr (TAN) racc += rt;             // jvp:178
-        v8bf pb[2][NI], hb[2][NI];
+        constexpr bool HLO = TAN && !X3 && QA_JVP_HLO;
+        v8bf pb[2][NI], hb[2][NI], hlo[2];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          v4u pp[NI], hp[NI];
+          v4u pp[NI], hp[NI], hl;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float p0 = p[8 * s + 2 * j], p1 = p[8 * s + 2 * j + 1];
             const float h0 = hh[8 * s + 2 * j], h1 = hh[8 * s + 2 * j + 1];
             pp[0][j] = pk_bf16(p0, p1);
             if constexpr (TAN) hp[0][j] = pk_bf16(h0, h1);
+            if constexpr (HLO)
+              hl[j] = pk_bf16(h0 - __uint_as_float(hp[0][j] << 16), h1 - __uint_as_float(hp[0][j] & 0xffff0000u));
             if constexpr (X3) {
               pp[1][j] = pk_bf16(p0 - __uint_as_float(pp[0][j] << 16), p1 - __uint_as_float(pp[0][j] & 0xffff0000u));
               if constexpr (TAN)
@@ -234,6 +245,7 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
             pb[s][x] = __builtin_bit_cast(v8bf, pp[x]);
             hb[s][x] = __builtin_bit_cast(v8bf, hp[x]);
           }
+          if constexpr (HLO) hlo[s] = __builtin_bit_cast(v8bf, hl);
         }
 #pragma unroll
         for (int b = 0; b < C::NDB; ++b) {
@@ -249,6 +261,7 @@ __global__ __launch_bounds__(256, 1) void jvp_fwd_kernel(JvpArgs a) {
             if constexpr (TAN) {
               ab[b] = mm(tva, pb[s], ab[b]); // jvp:173-174
               ab[b] = mm(va, hb[s], ab[b]);  // jvp:180-181
+              if constexpr (HLO) ab[b] = mfma_bf16(va[0], hlo[s], ab[b]);
             }
           }
         }

@@ -1,12 +1,12 @@
 """Kernels of one int8 fwd+bwd step at config 3 in launch order, with durations and the idle gaps
 between them (dev tool; run under rocprofv3 --kernel-trace --output-format csv, then
-python tools/step_trace.py --report <kernel_trace.csv>); --causal for the causal step."""
+python tools/step_trace.py --report <kernel_trace.csv>); --causal for the causal step, --bf16 for the bf16 step."""
 import csv
 import os
 import sys
 
 
-def run(causal=False):
+def run(causal=False, bf16=False):
     import torch
     sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
     from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward
@@ -19,6 +19,17 @@ def run(causal=False):
         O, lse, qi, kiT, vi, sq, sk, sv, km, qb_, kb_ = _int8_forward(q, k, v, smooth=True, images=True,
                                                                        causal=causal)
         _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb_, kb_, causal=causal)
+    if bf16:   # the bench's bf16 step (k-mean marker launched first so --report finds the step)
+        from quantizedattention_amd import _lib
+        from quantizedattention_amd.attention_bf16 import (helion_atten_bf16_fwd_training,
+                                                           helion_flash_atten_2_algo_4_bwd)
+        vb, dOf = v.bfloat16(), dO.float()
+        km = torch.empty((B, H, 1, D), dtype=torch.float16, device="cuda")
+
+        def step():
+            _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(km), B * H, S, D, _lib.stream_of(k))
+            O, lse = helion_atten_bf16_fwd_training(q, k, vb, causal)
+            helion_flash_atten_2_algo_4_bwd(q, k, vb, O, lse, causal, dOf)
     for _ in range(6):
         step()
     torch.cuda.synchronize()
@@ -45,4 +56,4 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--report":
         report(sys.argv[2])
     else:
-        run(causal="--causal" in sys.argv)
+        run(causal="--causal" in sys.argv, bf16="--bf16" in sys.argv)
