@@ -146,3 +146,22 @@ def test_int8_bwd_ws_bit_identical_large(lib):
     for name, x, y in zip(("dq", "dk", "dv"), a, b):
         assert torch.isfinite(x).all() and x.abs().max().item() > 0, name
         assert torch.equal(x, y), name
+
+
+@pytest.mark.parametrize("shape,causal", [((2, 6, 3, 256, 256, 64), True), ((1, 8, 2, 512, 512, 128), True),
+                                          ((2, 4, 4, 256, 256, 128), False)])
+def test_int8_bwd_run_to_run_identical(lib, shape, causal):
+    """The record backward repeated 8 times gives bit-identical dq, dk, dv (no atomics, one writer
+    per record and output tile): a guard against ring / wait-count races, which show up as
+    run-to-run differences (tools/race_check.py)."""
+    from quantizedattention_amd.attention_int8 import _int8_backward, helion_atten_int8_hl_dot_fwd
+    B, Hq, Hkv, Sq, Sk, D = shape
+    q, k, v = _inputs(shape, seed=9)
+    dO = torch.randn((B, Hq, Sq, D), generator=torch.Generator().manual_seed(10)).half().cuda()
+    O, lse, qi, kiT, vi, sq, sk, sv, _, _ = helion_atten_int8_hl_dot_fwd(
+        q.cuda() * 2, k.cuda() * 2, v.cuda(), causal=causal)
+    ref = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, causal=causal, kv_heads=Hkv, use_ws=True)
+    for _ in range(7):
+        out = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, causal=causal, kv_heads=Hkv, use_ws=True)
+        for name, a, b in zip(("dq", "dk", "dv"), out, ref):
+            assert torch.equal(a, b), name
