@@ -27,6 +27,8 @@
 // images, bf16 transposed k image) the same way; keys in registers, query on the lane.  Both compute
 // each (q-tile, k-tile) dS tile with the same operation order, so tile scales and dS_i8 agree bit
 // for bit.  Tile-wide maxima use DPP + permlane reductions.  No atomics: deterministic.
+#include <climits>
+
 #include "common.h"
 
 namespace qattn {
@@ -378,6 +380,10 @@ void int8_bwd_kernel(
       c1 = sy_a * (sxaw * qks);
       c2 = sy_b * sxbw;
     }
+    // key > query as one compare per score against an immediate: dd = key - (first query of the
+    // lane's row group), INT_MIN off the diagonal tiles (nothing masked there)
+    const int dd = !diag ? INT_MIN
+                         : (ROLE == ROLE_DQ ? (y0 + 4 * h) - (x0 + c32) : (x0 + c32) - (y0 + 4 * h));
     if constexpr (G::HAS_LD) {
       const float* ld = reinterpret_cast<const float*>(slot(t) + G::LDO);
 #pragma unroll
@@ -390,7 +396,7 @@ void int8_bwd_kernel(
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
           float p = exp2_f32(fmaf((float)sa[i], c1, -lse_r[j]));
-          if (diag && x0 + c32 > y0 + 8 * g + 4 * h + j) p = 0.f;   // key > query
+          if (CAUSAL && dd > 8 * g + j) p = 0.f;   // key > query: x0 + c32 > y0 + 8g + 4h + j
           if constexpr (G::WANT_P) P[i] = p;
           if constexpr (G::WANT_DS) dS[i] = p * fmaf((float)pa[i], c2, -d_r[j]);
         }
@@ -401,7 +407,8 @@ void int8_bwd_kernel(
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float p = exp2_f32(fmaf((float)sa[i], c1, -lsex));
-        if (diag && y0 + (i & 3) + 8 * (i >> 2) + 4 * h > x0 + c32) p = 0.f;   // key > query
+        // key > query: y0 + (i & 3) + 8 (i >> 2) + 4h > x0 + c32
+        if (CAUSAL && dd > -((i & 3) + 8 * (i >> 2))) p = 0.f;
         dS[i] = p * fmaf((float)pa[i], c2, -Dx);
       }
     }
