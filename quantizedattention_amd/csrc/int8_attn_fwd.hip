@@ -307,9 +307,12 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     const bool diag = CAUSAL && (t * C::KT + C::KT - 1 > q0 + qoff);
     v16i acc = acc_in;
     if (diag) {
+      // key > query as one compare per score against an immediate:
+      // t KT + (r & 3) + 8 (r >> 2) + 4h > q0 + qoff + c32  <=>  dd > -((r & 3) + 8 (r >> 2))
+      const int dd = t * C::KT + 4 * h - (q0 + qoff + c32);
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (t * C::KT + (r & 3) + 8 * (r >> 2) + 4 * h > q0 + qoff + c32) acc[r] = INT_MIN;
+        if (dd > -((r & 3) + 8 * (r >> 2))) acc[r] = INT_MIN;
     }
     int mx = imax3(acc[0], acc[1], acc[2]);
     mx = imax3(mx, acc[3], acc[4]);
