@@ -59,11 +59,14 @@ def _check_shapes(q, k, v):
         raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
 
 
-# P.V contraction of the forward (csrc/int8_attn_fwd.hip):
-#   "i8" (default): v_mfma_i32_32x32x32_i8 on P_i8 x v_i8, as the reference's hl.dot (int8:249), with
-#         one fused dequantisation per 32-key tile; measured the faster mode;
-#   "f16": v_mfma_f32_32x32x16_f16 on f16(P_i8 * sp) x f16(v_i8 * sv), the tile scale in the operands.
-# Same P_i8, scales and tolerance either way; QATTN_INT8_PV selects the default.
+# P.V contraction of the forward (csrc/int8_attn_fwd.hip, csrc/int8_attn_fwd_rs.hip):
+#   "i8": v_mfma_i32_32x32x32_i8 on P_i8 x v_i8, as the reference's hl.dot (int8:249), with one fused
+#         dequantisation per 32-key tile;
+#   "f16": v_mfma_f32_32x32x16_f16 on f16(P_i8 * sp) x f16(v_i8 * sv), the tile scale in the operands;
+#   "rs": the f16 contraction in the role-split kernel (one MFMA wave and two softmax waves per SIMD)
+#         where it applies (non-causal, head_dim 128), "i8" elsewhere.
+# Same P_i8, scales and tolerance in every mode; QATTN_INT8_PV selects the default.
+PV_MODES = ("i8", "f16", "rs")
 PV_MODE = os.environ.get("QATTN_INT8_PV", "i8")
 
 
@@ -76,8 +79,8 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     ``images``, else None).  ``pv``: the P.V mode ("f16" / "i8", default PV_MODE).
     """
     pv = PV_MODE if pv is None else pv
-    if pv not in ("f16", "i8"):
-        raise _lib.QAttnError(f"qattn int8: unknown P.V mode {pv!r} (f16 or i8)")
+    if pv not in PV_MODES:
+        raise _lib.QAttnError(f"qattn int8: unknown P.V mode {pv!r} (one of {PV_MODES})")
     _check_shapes(q, k, v)
     _lib.require_gpu(q, k, v)
     q = q.to(torch.float16).contiguous()
@@ -85,6 +88,8 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     v = v.to(torch.float16).contiguous()
     B, H, S, D = q.shape
     Hkv, Sk = k.shape[1], k.shape[2]
+    if pv == "rs" and (causal or D != 128):
+        pv = "i8"
     N = B * H * S
     Nkv = B * Hkv * Sk
     dev = q.device
@@ -96,7 +101,7 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     sk = torch.empty((Nkv // BKV,), dtype=torch.float16, device=dev)
     sv = torch.empty((Nkv // BKV,), dtype=torch.float16, device=dev)
     # P.V operand image of v: f16(v_i8 * sv) ("f16") or the int8 V^T operand image ("i8")
-    vop = torch.empty((Nkv, D), dtype=torch.float16 if pv == "f16" else torch.int8, device=dev)
+    vop = torch.empty((Nkv, D), dtype=torch.int8 if pv == "i8" else torch.float16, device=dev)
     O = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
     lse = torch.empty((N,), dtype=torch.float16, device=dev)
     q_bf = k_bf = None
@@ -112,7 +117,12 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
               _lib.ptr(k_mean), Nkv, Sk, D, st)
     qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
-    if pv == "f16":
+    if pv == "rs":
+        _lib.call("qattn_int8_quant_vop", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), Nkv,
+                  D, st)
+        _lib.call("qattn_int8_attn_fwd_rs", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
+                  _lib.ptr(vop), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, D, qks, st)
+    elif pv == "f16":
         _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), None,
                   Nkv, Sk, D, st)
         _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
@@ -197,8 +207,10 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
     dv = torch.empty((B, Hkv, Sk, D), dtype=torch.float16, device=dev)
     qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
     sms = float(torch.tensor(1.0 / math.sqrt(D), dtype=torch.float32))
-    common = (_lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8), _lib.ptr(sq.contiguous()), _lib.ptr(k_i8),
-              _lib.ptr(sk.contiguous()), _lib.ptr(v_i8), _lib.ptr(sv.contiguous()), _lib.ptr(LD),
+    # (contiguous copies bound to names: they must outlive the launches that read them)
+    sq, sk, sv = sq.contiguous(), sk.contiguous(), sv.contiguous()
+    common = (_lib.ptr(dO_i8), _lib.ptr(sdO), _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8),
+              _lib.ptr(sk), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(LD),
               _lib.ptr(q_bf), _lib.ptr(k_bf), _lib.ptr(dO_bf), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv))
     shape = (B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, sms, st)
     chunk = _ws_chunk(ws_chunk, causal, B * Hkv, Sk)

@@ -75,7 +75,11 @@ def _jvp(q_fp32_input, k_fp32_input, v_fp32_input, tangents):
     if all(t.dtype == torch.bfloat16 for t in ins):
         if k_tokens % 64:
             raise _lib.QAttnError("qattn jvp: k tokens must be a multiple of 64 for bf16 inputs")
-        ptrs = [_lib.ptr(t.contiguous()) for t in ins]
+        # keep the contiguous copies alive through the launch: a copy freed as soon as its address
+        # is taken hands its block to the next input's copy (the caching allocator), and the
+        # kernel would read the wrong tensor
+        xs = [t.contiguous() for t in ins]
+        ptrs = [_lib.ptr(t) for t in xs]
         if tangents is None:
             _lib.call("qattn_jvp_primal_ex", *ptrs, _lib.ptr(O), _lib.ptr(lse), *shape)
         else:

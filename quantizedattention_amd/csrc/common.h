@@ -28,6 +28,7 @@ typedef short v8s __attribute__((ext_vector_type(8)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef int v2i __attribute__((ext_vector_type(2)));
 
 #define QA_DEVICE __device__ __forceinline__
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))

@@ -189,7 +189,8 @@ __global__ __launch_bounds__(256) void probe_quant_div_kernel(int s_lo, int s_hi
         // bad[0]: count; bad[1..5]: the first mismatch (s bits, x bits, reference, byte, image bits)
         if (atomicAdd(bad, 1u) == 0) {
           bad[1] = (unsigned)sb;
-          bad[2] = (unsigned)__builtin_bit_cast(unsigned short, x[j]);
+          const _Float16 xj = x[j];   // (not bit_cast of the element lvalue: hipcc folds it to x[0])
+          bad[2] = (unsigned)__builtin_bit_cast(unsigned short, xj);
           bad[3] = (unsigned)ref[j];
           bad[4] = (unsigned)byte;
           bad[5] = __float_as_uint(qf[j]);

@@ -85,14 +85,22 @@ class QuantizedKV:
             B, H, S, D = self.shape
             _lib.require_gpu(self.v_i8)
             out = torch.empty((B * H * S, D), dtype=torch.int8, device=self.v_i8.device)
-            _lib.call("qattn_int8_v_image", _lib.ptr(self.v_i8.contiguous()), _lib.ptr(out), B * H * S, D,
+            vi = self.v_i8.contiguous()   # (bound: it must outlive the launch)
+            _lib.call("qattn_int8_v_image", _lib.ptr(vi), _lib.ptr(out), B * H * S, D,
                       _lib.stream_of(self.v_i8))
             self._vt = out
         return self._vt
 
     def operand(self, pv: str) -> torch.Tensor:
-        """The P.V operand of mode ``pv`` ("f16" or "i8", attention_int8.PV_MODE)."""
-        return self.vdq() if pv == "f16" else self.vt()
+        """The P.V operand of mode ``pv`` ("f16": f16(v_i8 * sv); "i8" / "rs": the int8 V^T image --
+        the role-split forward is a training-shape kernel, a cache runs the int8 decoding path)."""
+        return self.vdq() if _pv_mode(pv) == "f16" else self.vt()
+
+    def drop_operands(self) -> None:
+        """Free the cached P.V operand images (rebuilt on the next use); the cache proper is k_i8,
+        v_i8, sk, sv (and k_mean)."""
+        self._vdq = None
+        self._vt = None
 
     # ------------------------------------------------------------------------------ growth
     def append(self, k: torch.Tensor, v: torch.Tensor) -> "QuantizedKV":
@@ -196,13 +204,22 @@ def quantize_kv(k: torch.Tensor, v: torch.Tensor, smooth: bool = True,
     v_i8 = torch.empty((B, H, S, D), dtype=torch.int8, device=dev)
     sk = torch.empty((N // BLOCK,), dtype=torch.float16, device=dev)
     sv = torch.empty((N // BLOCK,), dtype=torch.float16, device=dev)
-    vdq = torch.empty((N, D), dtype=torch.float16, device=dev)
     km = None if k_mean is None else k_mean.to(torch.float16).contiguous()
     _lib.call("qattn_int8_quant", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(km), N, S, D,
               st)
-    _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vdq), None, N, S,
-              D, st)
-    return QuantizedKV(k_i8, v_i8, sk, sv, km, vdq)
+    # v: indices, scales and the P.V operand image of the default (int8) mode in one pass, 1 B per
+    # element; the f16 image (2 B per element) is built only if the f16 mode asks for it
+    vt = torch.empty((N, D), dtype=torch.int8, device=dev)
+    _lib.call("qattn_int8_quant_vt", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vt), N, D, st)
+    return QuantizedKV(k_i8, v_i8, sk, sv, km, None, vt)
+
+
+def _pv_mode(pv):
+    from . import attention_int8
+    pv = attention_int8.PV_MODE if pv is None else pv
+    if pv not in attention_int8.PV_MODES:
+        raise _lib.QAttnError(f"qattn kv cache: unknown P.V mode {pv!r} (one of {attention_int8.PV_MODES})")
+    return "i8" if pv == "rs" else pv
 
 
 def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False, pv=None):
@@ -212,13 +229,12 @@ def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False
     are the LAST Sq positions (query i keeps keys <= Sk - Sq + i), Sq <= Sk.  Returns (O fp16
     [B, Hq, Sq, D], lse fp16 [B*Hq*Sq]); without ``causal`` identical to the forward on the un-cached
     tensors (bit-identical when one key split covers the cache).  ``pv``: the P.V mode (default
-    attention_int8.PV_MODE).
+    attention_int8.PV_MODE; "rs" runs as "i8" here).
     Non-causal with the int8 P.V at head_dim 128 runs in the decoding layout (_decode_split: the
     grouped query heads of a key/value head in one workgroup, long caches split over the keys and
     merged); the results equal the one-pass forward's up to the merge's rounding (<= 2e-3).
     """
-    from . import attention_int8
-    pv = attention_int8.PV_MODE if pv is None else pv
+    pv = _pv_mode(pv)
     B, Hkv, Sk, D = kv.shape
     if q.dim() != 4 or q.shape[0] != B or q.shape[3] != D or q.shape[1] % Hkv or q.shape[2] % BLOCK:
         raise _lib.QAttnError("qattn kv cache: q must be [B, G*Hkv, 32*n, D] for the cache's B, Hkv, D")
