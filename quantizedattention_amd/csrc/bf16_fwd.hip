@@ -305,8 +305,7 @@ extern "C" int qattn_bf16_fwd_ex(const void* q, const void* k, const void* v, vo
   {                                                                                              \
     using C = Bf16FwdCfg<Dv>;                                                                    \
     const int nq = (int)((sq + C::QROWS - 1) / C::QROWS);                                        \
-    hipFuncSetAttribute((const void*)bf16_fwd_kernel<Dv, CV>,                                    \
-                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);                     \
+    { static int granted_ = 0; lds_grant((const void*)bf16_fwd_kernel<Dv, CV>, C::LDS, granted_); }                     \
     hipLaunchKernelGGL((bf16_fwd_kernel<Dv, CV>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), \
                        C::LDS, st, (const _Float16*)q, (const _Float16*)k, (const __bf16*)v,     \
                        (float*)out, (float*)lse, (int)bh, (int)sq, (int)sk, group, qks);         \

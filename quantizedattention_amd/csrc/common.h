@@ -33,6 +33,18 @@ typedef int v2i __attribute__((ext_vector_type(2)));
 #define QA_DEVICE __device__ __forceinline__
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
+// ---------------------------------------------------------------- host: dynamic-LDS grants
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) only when a launch needs more dynamic LDS than
+// the kernel was granted so far: `granted` is a static of the calling launch function (one per
+// kernel instantiation), so steady-state launches (decode steps of ~50 us) make no attribute call.
+inline bool lds_grant(const void* kernel, int bytes, int& granted) {
+  if (bytes <= granted) return true;
+  if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+    return false;
+  granted = bytes;
+  return true;
+}
+
 // ---------------------------------------------------------------- MFMA wrappers
 QA_DEVICE v16i mfma_i8(v4i a, v4i b, v16i c) {
   return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
@@ -290,6 +302,24 @@ QA_DEVICE void fma_mix16_after(const v16i& acc, float c, float n, int dep, v2h* 
 #pragma unroll
   for (int j = 0; j < 8; ++j) d[j] = __builtin_bit_cast(v2h, r[j]);
 }
+// The same S = f16(X c) from a biased accumulator through f32: one v_pk_fma_f32 per pair (the
+// exact (KMAG + X) c - KMAG c, rounded to f32) and one v_cvt_pk_f16_f32 (RNE).  Two roundings (f32,
+// then f16) where fma_mix16_after has one: the f16 results differ only where f32(X c) lands on an
+// f16 rounding midpoint.  Issue cost ~12.9 cycles per pair against ~16.7 for two v_fma_mix{lo,hi}
+// (tools/ubench/coexec2.py: v_fma_mix*_f16 issue like transcendentals, ~8.4 cycles).  Compiler
+// builtins, so hipcc inserts the MFMA-result -> VALU wait states itself.
+QA_DEVICE void biased_to_f16x16(const v16i& acc, float c, float nb, v2h* d) {
+  const v2f_ c2 = {c, c}, n2 = {nb, nb};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const v2f_ a = {__int_as_float(acc[2 * j]), __int_as_float(acc[2 * j + 1])};
+    d[j] = __builtin_convertvector(__builtin_elementwise_fma(a, c2, n2), v2h);
+  }
+}
+QA_DEVICE _Float16 biased_to_f16(int a, float c, float nb) {
+  return (_Float16)__builtin_fmaf(__int_as_float(a), c, nb);
+}
+
 // f32(x.lo) + f32(x.hi) of a packed f16 pair in one v_fma_mix_f32
 QA_DEVICE float pk_hsum(v2h x) {
   float r;

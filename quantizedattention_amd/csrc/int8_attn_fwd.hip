@@ -197,6 +197,8 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     // causal tiles crossing this wave's diagonal: keys above the row's query drop out of the max
     // (INT_MIN) and get d = -inf below, so P = 0 and the tile scale ignores them
     const bool diag = CAUSAL && (t * C::KT + C::KT - 1 > q0 + qoff);
+    // QA_FWD_LITERAL_P: the reference's literal P_i8 chain on every tile (priced)
+    const bool lit = diag || (QA_FWD_LITERAL_P != 0);
     v16i acc = acc_in;
     if (diag) {
       // key > query as one compare per score against an immediate:
@@ -224,8 +226,13 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     if constexpr (C::QK_BIAS) {   // on the biased accumulator: one v_fma_mix per score
       const float c = kmag_scale(cq * ck_lds[t]);
       const float nb = -KMAG * c;
+#if QA_FWD_S_PK
+      rm = biased_to_f16(mx, c, nb);
+      biased_to_f16x16(acc, c, nb, s2);
+#else
       rm = fma_mix1(__int_as_float(mx), c, nb);
       fma_mix16_after(acc, c, nb, mx, s2);
+#endif
     } else {
       const float c = cq * ck_lds[t];
       rm = (_Float16)((float)mx * c);
@@ -236,7 +243,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     const v2h rm2 = {rm, rm};
 #pragma unroll
     for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;   // f16(S - rm)  (int8:211, 232-236)
-    if constexpr (CAUSAL) {
+    if constexpr (CAUSAL || QA_FWD_LITERAL_P) {
       // Diagonal tiles keep few keys per row, where one P_i8 step weighs much in O: there P_i8
       // follows the reference chain literally (int8:205-237): next_m = max(m, rm) with the
       // undeferred running max, P = exp2(f32(f16(S - next_m))), sp = exp2(f32(f16(rm - next_m)))/127
@@ -245,8 +252,8 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       const bool kept = mx != INT_MIN;     // the row keeps a key of this tile
       const _Float16 nm_ref = (kept && rm > mt) ? rm : mt;
       if (kept) mt = nm_ref;
-      st.diag = diag;
-      if (diag) {
+      st.diag = lit;
+      if (lit) {
         const float spr = exp2_f32((float)(_Float16)((float)rm - (float)nm_ref)) / 127.0f;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
@@ -296,7 +303,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     // row sum of e: packed f16 adds (pairs, then sums of 4 and 8 values <= 8), one f32 mix-add
     const v2h s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
     l = fmaf(pk_hsum(s), st.er, l);
-    if (CAUSAL && st.diag) {   // the literal-chain P_i8 of a diagonal tile (sm1)
+    if ((CAUSAL || QA_FWD_LITERAL_P) && st.diag) {   // the literal-chain P_i8 of the tile (sm1)
       if constexpr (PV == PV_F16) {
         const _Float16 sp = (_Float16)st.cpv;
         const v2h sp2 = {sp, sp};
@@ -440,8 +447,7 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
   using C = Int8FwdCfg<D, PV>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int lds = C::RING + (int)(((sk_tok / 32) * 4 * (PV == PV_I8 ? 2 : 1) + 15) / 16 * 16);
-  hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<D, PV, CAUSAL>,
-                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  { static int granted_ = 0; lds_grant((const void*)int8_attn_fwd_kernel<D, PV, CAUSAL>, lds, granted_); }
   hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV, CAUSAL>), dim3((unsigned)(nq * bh)),
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
                      (const int8_t*)k_i8, (const _Float16*)sk, vop, (const _Float16*)sv,
@@ -490,8 +496,7 @@ static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, 
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int nsplit = (int)((sk_tok + ks - 1) / ks);
   const int lds = C::RING + (int)(((ks / 32) * 8 + 15) / 16 * 16);
-  hipFuncSetAttribute((const void*)int8_attn_fwd_kernel<D, PV_I8, false, true>,
-                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  { static int granted_ = 0; lds_grant((const void*)int8_attn_fwd_kernel<D, PV_I8, false, true>, lds, granted_); }
   hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV_I8, false, true>), dim3((unsigned)(nq * bh), (unsigned)nsplit),
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
                      (const int8_t*)k_i8, (const _Float16*)sk, vt, (const _Float16*)sv, (_Float16*)opart,

@@ -45,6 +45,23 @@
 
 namespace qattn {
 
+// Diagnostic build only (-DQA_RS_STAMP=1, tools/rs_stamps.py): s_memtime stamps at the phase
+// boundaries of steps 40..47 of workgroup 777, lanes 0 of waves 0 and NM (a matrix and a softmax
+// wave), written with vector stores to a buffer of their own that no other code reads.
+#ifndef QA_RS_STAMP
+#define QA_RS_STAMP 0
+#endif
+#if QA_RS_STAMP
+__device__ unsigned long long g_rs_stamp[2][8][16];
+#define RS_STAMP(role, k)                                                                       \
+  do {                                                                                          \
+    if (blockIdx.x == 777 && s_st >= 40 && s_st < 48 && (tid & 63) == 0)                         \
+      g_rs_stamp[role][s_st - 40][k] = __builtin_amdgcn_s_memtime();                            \
+  } while (0)
+#else
+#define RS_STAMP(role, k) do { } while (0)
+#endif
+
 // MPS = matrix waves per SIMD: 1 (4 matrix + 8 softmax waves, 128 query rows per workgroup) or 2
 // (8 matrix + 4 softmax waves, 256 rows: half the K/V stream per row, tools/ab_rs.py)
 template <int D, int MPS>
@@ -249,17 +266,21 @@ __global__ __launch_bounds__((RsCfg<D, MPS>::THREADS), 3) void int8_attn_fwd_rs_
     // for the next step.  A matrix wave past the last query row (active false) computes on whatever
     // its buffers hold: nothing reads its S tiles (its softmax waves idle) and its O is not stored.
     auto step = [&](int s, bool qk, bool pv, bool pre_k, bool pre_v) {
+      [[maybe_unused]] const int s_st = wave == 0 ? s : -1;
+      RS_STAMP(0, 0);
       if (qk && !(QA_RS_ABL & 4)) {
         sacc = mfma_i8(kf[0], qf[0], sacc);
 #pragma unroll
         for (int ks = 1; ks < C::NKS; ++ks) sacc = mfma_i8(kf[ks], qf[ks], sacc);
       }
       __builtin_amdgcn_sched_barrier(0);
+      RS_STAMP(0, 1);
       if (pv) {
         const char* pb = pbuf + (s & 1) * C::TILE + l16;   // P(s-2): buffer (s-2) & 1
         const v8h p0 = *reinterpret_cast<const v8h*>(pb);
         const v8h p1 = *reinterpret_cast<const v8h*>(pb + 1024);
         const float r = rbuf[(s & 1) * 32 + c32];
+        RS_STAMP(0, 2);
         if (!(QA_RS_ABL & 1) && __ballot(r != 1.0f) != 0) {
           asm volatile("" ::: "memory");   // (rare: keep it a branch)
 #pragma unroll
@@ -273,6 +294,7 @@ __global__ __launch_bounds__((RsCfg<D, MPS>::THREADS), 3) void int8_attn_fwd_rs_
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+      RS_STAMP(0, 3);
       if (qk && !(QA_RS_ABL & 4)) {
         // S = f16(X c), c = sq sk qks (int8:200-203), on the biased accumulator
         const float c = kmag_scale(cq * ck_lds[s]);
@@ -286,13 +308,21 @@ __global__ __launch_bounds__((RsCfg<D, MPS>::THREADS), 3) void int8_attn_fwd_rs_
           *reinterpret_cast<v2u*>(sb + 512 * g) =
               v2u{__builtin_bit_cast(unsigned, s2[2 * g]), __builtin_bit_cast(unsigned, s2[2 * g + 1])};
       }
+      // the S tile must be in LDS before the barrier; the fragment prefetches for the next step need
+      // not: they stay in flight across it (the compiler waits for them where they are used, and
+      // their ring slots are refilled only steps later)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      RS_STAMP(0, 4);
       if (pre_k) k_load(s + 1, kf);
       if (pre_v) v_load(s - 1, va);
       if (qk) kmag_seed(sacc);
       const int tn = s + C::LOOK;
       if (dw && !(QA_RS_ABL & 8)) dma.issue(smem_lds + (tn % C::NSLOT) * C::SLOT, min(tn, nt - 1), mw);
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::VMCNT) : "memory");
+      RS_STAMP(0, 5);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::VMCNT) : "memory");
+      RS_STAMP(0, 6);
+      asm volatile("s_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     };
 
@@ -363,6 +393,8 @@ __global__ __launch_bounds__((RsCfg<D, MPS>::THREADS), 3) void int8_attn_fwd_rs_
     }
     // one tile of every unit, phase by phase over the units (independent chains side by side)
     auto sm = [&](int j) {
+      [[maybe_unused]] const int s_st = wave == C::NM ? j + 1 : -1;
+      RS_STAMP(1, 0);
       const int jb = (j & 1) * C::TILE;
       v2h x[C::UPV][4];
 #pragma unroll
@@ -397,6 +429,7 @@ __global__ __launch_bounds__((RsCfg<D, MPS>::THREADS), 3) void int8_attn_fwd_rs_
                                            __builtin_bit_cast(v2h, (unsigned)r32[1]));
         rm2[u] = __builtin_elementwise_max(rm2[u], __builtin_shufflevector(rm2[u], rm2[u], 1, 0));
       }
+      RS_STAMP(1, 1);
       // deferred running max per unit (16 rows): moves only when a row's tile max passes m + THR
       float rout[C::UPV];
       bool mv = false;
@@ -440,6 +473,7 @@ __global__ __launch_bounds__((RsCfg<D, MPS>::THREADS), 3) void int8_attn_fwd_rs_
           p_operand4(e, sp2, nsp2, w[u]);
         }
       }
+      RS_STAMP(1, 2);
 #pragma unroll
       for (int u = 0; u < C::UPV; ++u)
         *reinterpret_cast<v4u*>(pbu[u] + jb) =
@@ -449,7 +483,14 @@ __global__ __launch_bounds__((RsCfg<D, MPS>::THREADS), 3) void int8_attn_fwd_rs_
     rs_barrier_lds();   // step 0
     for (int j = 0; j < nt; ++j) {   // step j + 1
       if (any_act && !(QA_RS_ABL & 1)) sm(j);
-      rs_barrier_lds();
+      {
+        [[maybe_unused]] const int s_st = wave == C::NM ? j + 1 : -1;
+        RS_STAMP(1, 3);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        RS_STAMP(1, 4);
+        asm volatile("s_barrier" ::: "memory");
+        RS_STAMP(1, 5);
+      }
     }
     rs_barrier_lds();   // step nt + 1
     // {m, l} of each row: the four lanes of row q hold partial sums over their key groups
@@ -473,13 +514,8 @@ static int launch_fwd_rs(const void* q_i8, const void* sq, const void* k_i8, con
   using C = RsCfg<D, MPS>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int lds = C::lds_bytes(sk_tok);
-  static int lds_set = 0;   // the largest dynamic LDS size granted so far
-  if (lds > lds_set) {
-    if (hipFuncSetAttribute((const void*)int8_attn_fwd_rs_kernel<D, MPS>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-      return 2;
-    lds_set = lds;
-  }
+  static int granted = 0;
+  if (!lds_grant((const void*)int8_attn_fwd_rs_kernel<D, MPS>, lds, granted)) return 2;
   hipLaunchKernelGGL((int8_attn_fwd_rs_kernel<D, MPS>), dim3((unsigned)(nq * bh)), dim3(C::THREADS), lds,
                      st, (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
                      (const _Float16*)vop, (_Float16*)out, (_Float16*)lse, (int)bh, (int)sq_tok,
@@ -509,3 +545,9 @@ extern "C" int qattn_int8_attn_fwd_rs(const void* q_i8, const void* sq, const vo
   return launch_fwd_rs<128, QA_RS_MPS>(q_i8, sq, k_i8, sk, vop, out, lse, bh, sq_tok, sk_tok, group, qks,
                                        (hipStream_t)stream);
 }
+
+#if QA_RS_STAMP
+extern "C" int qattn_rs_stamps(void* host_dst) {
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(qattn::g_rs_stamp), sizeof(qattn::g_rs_stamp)) == hipSuccess ? 0 : 2;
+}
+#endif

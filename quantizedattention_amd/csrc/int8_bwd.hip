@@ -849,8 +849,7 @@ static void launch_bwd_c(const void* x8a, const void* x8b, const void* sxa, cons
   using G = BwdCfg<D, ROLE>;
   const int lds = G::NSLOT * G::SLOT + (int)((2 * (ny / 32) * 2 + 15) / 16 * 16) +
                   (WS ? G::WAVES * (int)(ny / 32) * 4 : 0);
-  hipFuncSetAttribute((const void*)int8_bwd_kernel<D, ROLE, CAUSAL, WS>,
-                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  { static int granted_ = 0; lds_grant((const void*)int8_bwd_kernel<D, ROLE, CAUSAL, WS>, lds, granted_); }
   const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
   hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE, CAUSAL, WS>), dim3((unsigned)(nb * bhx)),
                      dim3(64 * G::WAVES), lds, st, (const int8_t*)x8a, (const int8_t*)x8b,
@@ -880,8 +879,7 @@ static void launch_dqw_c(const void* ds8, const void* sds, const void* k_bf, con
   using G = DqwCfg<D>;
   const int nkt = (int)(skt / 32);
   const int lds = G::RBASE + G::RSLOT * G::REC + G::WAVES * nkt * 4 + (nkt * 2 + 15) / 16 * 16;
-  hipFuncSetAttribute((const void*)int8_bwd_dqw_kernel<D, CAUSAL>,
-                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  { static int granted_ = 0; lds_grant((const void*)int8_bwd_dqw_kernel<D, CAUSAL>, lds, granted_); }
   const int nb = (int)((sqt + 32 * G::WAVES - 1) / (32 * G::WAVES));
   hipLaunchKernelGGL((int8_bwd_dqw_kernel<D, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
                      lds, st, (const int8_t*)ds8, (const float*)sds, (const __bf16*)k_bf,
@@ -1025,8 +1023,11 @@ extern "C" int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const 
 // dK+dV of a chunk writes its records into ws, the dQ pass of the same chunk reads them, and the next
 // chunk re-uses the same ws bytes.  Every tensor is head-major and contiguous, so a chunk is a plain
 // pointer offset; results are bit-identical to the one-shot call (each head's arithmetic is
-// unchanged).  A workspace of one chunk's records can stay resident in the 256 MB Infinity Cache
-// between its write and its read, instead of a full-problem workspace streaming through HBM twice.
+// unchanged).  The chunk size is the caller's: a chunk's records stay in the 256 MB Infinity Cache
+// between their write and their read only if the chunk's records plus the other bytes both passes
+// move stay under ~256 MB (MI355X_MICROARCH "Infinity Cache"); the default chunk at config 3 (32
+// heads, 539 MB of records) does not, so there the records go through HBM.  What chunking buys
+// there is a quarter of the workspace and a measured 2-4 % (attention_int8.WS_CHUNK).
 extern "C" int qattn_int8_attn_bwd_wsc(const void* dO_i8, const void* sdO, const void* q_i8,
                                        const void* sq, const void* k_i8, const void* sk,
                                        const void* v_i8, const void* sv, const void* LD,

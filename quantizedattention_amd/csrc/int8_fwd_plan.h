@@ -24,6 +24,21 @@ enum PvMode { PV_F16 = 0, PV_I8 = 1 };
 #ifndef QA_FWD_QK_BIAS
 #define QA_FWD_QK_BIAS -1
 #endif
+//   QA_FWD_S_PK     S = f16(X c) on the biased accumulator through v_pk_fma_f32 + v_cvt_pk_f16_f32
+//                   (1) instead of v_fma_mix{lo,hi}_f16 (0); common.h biased_to_f16x16.
+#ifndef QA_FWD_S_PK
+#define QA_FWD_S_PK 0
+#endif
+//   QA_FWD_LITERAL_P  1: every tile's P_i8 by the reference's literal chain (undeferred running max,
+//                   fp32 exp2, IEEE divisions), as the causal diagonal tiles always do; 0: only those.
+//   QA_FWD_THR      the deferred running max moves when a row's tile max exceeds it by more than
+//                   this (log2 units); 0 moves it on every increase, as the reference does.
+#ifndef QA_FWD_THR
+#define QA_FWD_THR 8.0f
+#endif
+#ifndef QA_FWD_LITERAL_P
+#define QA_FWD_LITERAL_P 0
+#endif
 
 template <int D, int PV>
 struct Int8FwdCfg {
@@ -51,7 +66,7 @@ struct Int8FwdCfg {
   // the ring, reused as the output staging area of the epilogue
   static constexpr int STAGE = WAVES * RowTile<D, _Float16>::BYTES;
   static constexpr int RING = NSLOT * SLOT > STAGE ? NSLOT * SLOT : STAGE;
-  static constexpr float THR = 8.0f;
+  static constexpr float THR = QA_FWD_THR;   // deferred running-max threshold (log2 units)
 };
 
 template <int D>
