@@ -160,13 +160,15 @@ def _ws_chunk(chunk, causal, bkv, sk):
 
 
 def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=None, causal=False,
-                   kv_heads=None, use_ws=None, ws_chunk=None, kv_len=None):
+                   kv_heads=None, use_ws=None, ws_chunk=None, kv_len=None, ws_poison=None):
     """Corrected int8 backward; q_bf / k_bf: bf16 images from the forward (computed here if None).
 
     kv_heads: key/value heads (default: those of O); their token count follows from k_i8T.
     use_ws: dQ from the dS workspace (True), by recomputation (False), or by size (None).
     ws_chunk: key/value heads per workspace chunk (None: WS_CHUNK / auto; 0 = all heads at once).
-    kv_len: key/value tokens, needed only to shape the (empty) gradients of an empty batch."""
+    kv_len: key/value tokens, needed only to shape the (empty) gradients of an empty batch.
+    ws_poison: a byte to fill the dS workspace with before the launch (protocol checks: every record
+    the dQ pass reads must have been written by the dK+dV pass, so results cannot depend on it)."""
     O = O.to(torch.float16).contiguous()
     dO = dO.to(torch.float16).contiguous()
     _lib.require_gpu(dO, O, q_i8)
@@ -228,6 +230,8 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
             ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
         except torch.cuda.OutOfMemoryError:
             ws = None   # no room for the workspace: recompute dS in the dQ pass (same results)
+        if ws is not None and ws_poison is not None:
+            ws.fill_(int(ws_poison) & 0xFF)
     if ws is not None and chunk < B * Hkv:
         _lib.call("qattn_int8_attn_bwd_wsc", *common, _lib.ptr(ws), chunk, *shape)
     elif ws is not None:

@@ -88,7 +88,11 @@ def sharded_forward(fn, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, gr
     """Run ``fn(q_loc, k_loc, v_loc) -> O_loc (or a tuple whose [0] is O)`` on this rank's slice of
     full [B, H, S, D] inputs and (optionally) all-gather O to every rank.  k and v may have fewer
     heads (grouped-query attention): each rank gets the key/value heads its query heads read
-    (:func:`kv_shard`), as [1, n / G, Sk, D].
+    (:func:`kv_shard`), as [1, n / G, Sk, D] (n key/value rows, one per query head, when its range
+    splits a group).
+
+    A shard that splits a group of query heads sharing a key/value head (uneven splits) runs with
+    one key/value copy per local query head instead.
 
     Returns (O_full or O_local as [B', H', S, D], the raw local result of ``fn``).
     """
@@ -98,12 +102,24 @@ def sharded_forward(fn, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, gr
     if k.shape[0] != B or v.shape[:2] != k.shape[:2]:
         raise ValueError("sharded_forward: k and v need q's batch and one head count")
     sh = shard_for(B, H, world, rank)
-    kvs = kv_shard(sh, H, k.shape[1])
     ql = local_slice(q, sh).unsqueeze(0)
-    kl, vl = (local_slice(t, kvs).unsqueeze(0) for t in (k, v))
+    Hkv = k.shape[1]
+    if H % Hkv:
+        raise ValueError(f"query heads {H} are not a multiple of key/value heads {Hkv}")
+    G = H // Hkv
+    if sh.bh0 % G == 0 and sh.bh1 % G == 0:
+        kvs = kv_shard(sh, H, Hkv)
+        kl, vl = (local_slice(t, kvs).unsqueeze(0) for t in (k, v))
+    else:
+        # the shard splits a group of query heads that share a key/value head: give every local
+        # query head its own copy of the key/value head it reads (group 1 locally; same results)
+        rows = torch.arange(sh.bh0, sh.bh1, device=k.device) // G
+        kl, vl = (t.reshape(B * Hkv, *t.shape[2:]).index_select(0, rows).unsqueeze(0) for t in (k, v))
     res = fn(ql.contiguous(), kl.contiguous(), vl.contiguous())
     O_loc = res[0] if isinstance(res, tuple) else res
-    if not gather or world == 1:
+    if world == 1:   # the one shard is the whole problem: hand it back in the caller's layout
+        return as_bhsd(O_loc.reshape(sh.n, S, -1), B, H), res
+    if not gather:
         return O_loc, res
     full, _ = all_gather_bh(O_loc.reshape(sh.n, S, -1), group=group)
     return as_bhsd(full, B, H), res

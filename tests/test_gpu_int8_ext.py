@@ -165,3 +165,32 @@ def test_int8_bwd_run_to_run_identical(lib, shape, causal):
         out = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, causal=causal, kv_heads=Hkv, use_ws=True)
         for name, a, b in zip(("dq", "dk", "dv"), out, ref):
             assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("shape,causal,chunk", [
+    ((2, 6, 3, 96, 96, 64), True, None), ((2, 6, 3, 160, 224, 64), False, 1),
+    ((1, 8, 2, 288, 288, 128), True, None), ((2, 4, 2, 416, 416, 128), False, 1),
+    ((1, 4, 4, 128, 384, 128), False, 2)])
+def test_int8_bwd_records_independent_of_workspace_contents(lib, shape, causal, chunk):
+    """The dS-record protocol, deterministically: the record backward runs twice, into workspaces
+    filled with 0x00 and with 0x7F before the launch, and once without records.  A dQ pass that read
+    a record the dK+dV pass had not written would see the fill pattern, so dq (and dk, dv) would
+    differ on the first run -- no repetition needed.  GQA, causal, Sq != Sk, partial workgroups
+    (Sq not a multiple of the 256-row dK+dV / dQ workgroups), one-pass and head-chunked records."""
+    from quantizedattention_amd.attention_int8 import _int8_backward, helion_atten_int8_hl_dot_fwd
+    B, Hq, Hkv, Sq, Sk, D = shape
+    g = torch.Generator().manual_seed(21)
+    q = torch.randn((B, Hq, Sq, D), generator=g)
+    k, v = (torch.randn((B, Hkv, Sk, D), generator=g) for _ in range(2))
+    dO = torch.randn((B, Hq, Sq, D), generator=g).half().cuda()
+    O, lse, qi, kiT, vi, sq, sk, sv, _, _ = helion_atten_int8_hl_dot_fwd(
+        q.cuda(), k.cuda(), v.cuda(), causal=causal)
+    kw = dict(causal=causal, kv_heads=Hkv, ws_chunk=chunk)
+    a = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, use_ws=True, ws_poison=0x00, **kw)
+    b = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, use_ws=True, ws_poison=0x7F, **kw)
+    c = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, use_ws=False, **kw)
+    torch.cuda.synchronize()
+    for name, x, y, z in zip(("dq", "dk", "dv"), a, b, c):
+        assert torch.isfinite(x).all() and x.abs().max().item() > 0, name
+        assert torch.equal(x, y), (name, "depends on the workspace fill")
+        assert torch.equal(x, z), (name, "records differ from recomputation")

@@ -107,7 +107,7 @@ def _worker(rank, world, port, B, H, S, D, errq, Hkv=None):
         raise
 
 
-@pytest.mark.parametrize("B,H,Hkv", [(2, 4, None), (1, 6, None), (2, 8, 2), (1, 8, 2)])
+@pytest.mark.parametrize("B,H,Hkv", [(2, 4, None), (1, 6, None), (2, 8, 2), (1, 8, 2), (1, 4, 1), (1, 6, 3)])
 def test_gloo_world2_sharded_forward(B, H, Hkv):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
