@@ -17,6 +17,7 @@ Other dtypes are cast to fp32 first.
 from __future__ import annotations
 
 import math
+import threading
 
 import torch
 
@@ -39,9 +40,14 @@ def helion_attention_jvp_forward_fp32(q_fp32_input, k_fp32_input, v_fp32_input,
                 (tan_q_fp32_input, tan_k_fp32_input, tan_v_fp32_input))
 
 
-def _jvp(q_fp32_input, k_fp32_input, v_fp32_input, tangents):
+# kernel launches by kind (tests count them: torch.func.jvp(attention_jvp, ...) is one launch)
+LAUNCHES = {"primal": 0, "tangent": 0}
+
+
+def _jvp(q_fp32_input, k_fp32_input, v_fp32_input, tangents, out_O=None):
     """The kernel call.  ``tangents`` None runs the primal-only kernel (qattn_jvp_primal_ex: O and
-    lse, bit-identical to the tangent kernel's) and returns (O, None, lse)."""
+    lse, bit-identical to the tangent kernel's) and returns (O, None, lse).  ``out_O``: write O into
+    this fp32 [B,H,S,D] contiguous tensor instead of a new one."""
     batch, head, q_tokens, q_head_dim = q_fp32_input.shape
     k_batch, k_head, k_tokens, k_head_dim = k_fp32_input.shape
     v_batch, v_head, v_tokens, v_head_dim = v_fp32_input.shape
@@ -65,7 +71,11 @@ def _jvp(q_fp32_input, k_fp32_input, v_fp32_input, tangents):
         raise _lib.QAttnError("qattn jvp: k and v need q's batch and a head count dividing q's")
     group = H // Hkv
     dev = q_fp32_input.device
-    O = torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+    if out_O is not None and (out_O.shape != (B, H, S, D) or out_O.dtype != torch.float32 or
+                              not out_O.is_contiguous() or out_O.device != dev):
+        raise _lib.QAttnError("qattn jvp: out_O must be a contiguous fp32 [B,H,S,D] tensor on q's device")
+    O = out_O if out_O is not None else torch.empty((B, H, S, D), dtype=torch.float32, device=dev)
+    LAUNCHES["primal" if tangents is None else "tangent"] += 1
     tO = torch.empty_like(O) if tangents is not None else None
     lse = torch.empty((B * H, S), dtype=torch.float32, device=dev)
     qks = float(torch.tensor(1.0 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
@@ -103,20 +113,46 @@ def _jvp(q_fp32_input, k_fp32_input, v_fp32_input, tangents):
 
 _plain = _lib.plain
 
+# Deferred forwards: when attention_jvp knows that the jvp rule will follow (a torch.func.jvp
+# transform, or forward-mode dual inputs), the Function's forward returns an EMPTY O and the jvp rule
+# fills it with the tangent kernel, which computes O and tO together: one launch per call.
+_DEFER = threading.local()
+
+
+def _key(q, k, v):
+    return (q.data_ptr(), k.data_ptr(), v.data_ptr(), tuple(q.shape), tuple(k.shape))
+
+
+def _jvp_follows(tensors) -> bool:
+    """True when the Function's jvp rule will run right after its forward: the innermost functorch
+    transform is torch.func.jvp, or (no functorch transform) an input is a forward-AD dual tensor."""
+    if torch._C._functorch.peek_interpreter_stack() is not None:
+        from torch._functorch.pyfunctorch import retrieve_current_functorch_interpreter
+        return retrieve_current_functorch_interpreter().key() == torch._C._functorch.TransformType.Jvp
+    import torch.autograd.forward_ad as fwAD
+    return any(fwAD.unpack_dual(t).tangent is not None for t in tensors)
+
 
 class AttentionJVP_autograd_function(torch.autograd.Function):
     """Attention O = softmax(q k^T / sqrt(D)) v whose forward-mode derivative is the kernel's tO.
 
     ``torch.func.jvp(attention_jvp, (q, k, v), (tq, tk, tv))`` and ``torch.autograd.forward_ad``
-    dual tensors both dispatch to :meth:`jvp`.  The forward runs the primal-only kernel
-    (qattn_jvp_primal_ex: no tangent chains, O bit-identical to the tangent kernel's), so a
-    ``torch.func.jvp`` call costs one primal and one tangent launch; reverse mode is not provided,
-    as in the reference, which has no backward for this path.
+    dual tensors both dispatch to :meth:`jvp`.  Called through :func:`attention_jvp` under either,
+    the forward defers O to the jvp rule's tangent kernel (one launch: O, tO and lse together);
+    called plainly it runs the primal-only kernel (qattn_jvp_primal_ex: no tangent chains, O
+    bit-identical to the tangent kernel's).  Reverse mode is not provided, as in the reference,
+    which has no backward for this path.
     """
 
     @staticmethod
     def forward(q, k, v):
         q, k, v = _plain(q), _plain(k), _plain(v)
+        if getattr(_DEFER, "on", False):
+            with torch._C._DisableFuncTorch():
+                B, H, S, D = q.shape
+                O = torch.empty((B, H, S, D), dtype=torch.float32, device=q.device)
+            _DEFER.pending = getattr(_DEFER, "pending", []) + [(_key(q, k, v), O)]
+            return O
         with torch._C._DisableFuncTorch():
             O, _tO, _lse = _jvp(q, k, v, None)
         return O
@@ -137,8 +173,16 @@ class AttentionJVP_autograd_function(torch.autograd.Function):
             tq = torch.zeros_like(q) if tq is None else tq.to(q.dtype)
             tk = torch.zeros_like(k) if tk is None else tk.to(k.dtype)
             tv = torch.zeros_like(v) if tv is None else tv.to(v.dtype)
+        # a deferred forward's O (see forward): filled here by the same launch as tO
+        out_O = None
+        pending = getattr(_DEFER, "pending", [])
+        for i, (key, O) in enumerate(pending):
+            if key == _key(q, k, v):
+                out_O = O
+                _DEFER.pending = pending[:i] + pending[i + 1:]
+                break
         with torch._C._DisableFuncTorch():   # plain allocations for the kernel's buffers
-            _O, tO, _lse = helion_attention_jvp_forward_fp32(q, k, v, tq, tk, tv)
+            _O, tO, _lse = _jvp(q, k, v, (tq, tk, tv), out_O=out_O)
         return tO
 
     @staticmethod
@@ -147,5 +191,11 @@ class AttentionJVP_autograd_function(torch.autograd.Function):
 
 
 def attention_jvp(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
-    """O fp32 [B,H,S,D]; differentiable in forward mode through the HIP tangent kernel."""
-    return AttentionJVP_autograd_function.apply(q, k, v)
+    """O fp32 [B,H,S,D]; differentiable in forward mode through the HIP tangent kernel (one launch
+    per torch.func.jvp / forward-AD call)."""
+    prev = getattr(_DEFER, "on", False)
+    _DEFER.on = _jvp_follows((q, k, v))
+    try:
+        return AttentionJVP_autograd_function.apply(q, k, v)
+    finally:
+        _DEFER.on = prev

@@ -69,10 +69,14 @@ def test_jvp_autograd_function_forward_mode(lib, dtype):
     g = torch.Generator().manual_seed(5)
     shape = (1, 2, 128, 64)
     q, k, v, tq, tk, tv = (torch.randn(shape, generator=g).to(dtype).cuda() for _ in range(6))
+    from quantizedattention_amd import attention_jvp as J
     O_ref, tO_ref, _ = helion_attention_jvp_forward_fp32(q, k, v, tq, tk, tv)
+    J.LAUNCHES.update(primal=0, tangent=0)
     O, tO = torch.func.jvp(attention_jvp, (q, k, v), (tq, tk, tv))
     torch.cuda.synchronize()
     assert torch.equal(O, O_ref) and torch.equal(tO, tO_ref)
+    # one launch per call: the forward defers O to the tangent kernel, which computes O and tO
+    assert J.LAUNCHES == {"primal": 0, "tangent": 1}, J.LAUNCHES
     with fwAD.dual_level():
         dq = fwAD.make_dual(q, tq)
         dk = fwAD.make_dual(k, tk)
@@ -80,6 +84,16 @@ def test_jvp_autograd_function_forward_mode(lib, dtype):
         out = attention_jvp(dq, dk, dv)
         p, t = fwAD.unpack_dual(out)
     assert torch.equal(p, O_ref) and torch.equal(t, tO_ref)
+    assert J.LAUNCHES == {"primal": 0, "tangent": 2}, J.LAUNCHES
+    # plain calls (no tangent anywhere) run the primal-only kernel; so do other transforms
+    assert torch.equal(attention_jvp(q, k, v), O_ref)
+    assert J.LAUNCHES == {"primal": 1, "tangent": 2}, J.LAUNCHES
+    with fwAD.dual_level():   # a dual on one input only: the other tangents are zeros
+        out = attention_jvp(fwAD.make_dual(q, tq), k, v)
+        p1, t1 = fwAD.unpack_dual(out)
+    O1, tO1, _ = helion_attention_jvp_forward_fp32(q, k, v, tq, torch.zeros_like(k), torch.zeros_like(v))
+    assert torch.equal(p1, O1) and torch.equal(t1, tO1)
+    assert J.LAUNCHES["primal"] == 1 and not getattr(J._DEFER, "pending", [])
     # matches forward-mode AD of the fp32 baseline within the mode's tolerance
     Ot, tOt = R.jvp_truth(*(x.float().cpu() for x in (q, k, v, tq, tk, tv)))
     tol = 1e-5 if dtype == torch.float32 else 1e-2
@@ -119,8 +133,8 @@ def test_jvp_grouped_query(lib, dtype, shape):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape", [(2, 4, 2, 256, 192, 128), (1, 2, 2, 96, 128, 64)])
 def test_jvp_primal_only_bit_identical(lib, dtype, shape):
-    """The primal-only kernel (the N1 Function's forward) returns the tangent kernel's O and lse
-    bit for bit: one primal + one tangent launch per torch.func.jvp call."""
+    """The primal-only kernel (the N1 Function's forward when no tangent follows) returns the tangent
+    kernel's O and lse bit for bit."""
     from quantizedattention_amd.attention_jvp import _jvp
     B, H, Hkv, Sq, Sk, D = shape
     g = torch.Generator().manual_seed(13)
