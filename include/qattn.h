@@ -112,6 +112,14 @@ int qattn_int8_attn_fwd_rs(const void* q_i8, const void* sq, const void* k_i8, c
                            const void* vop, void* out, void* lse, long bh, long sq_tok, long sk_tok,
                            int group, int head_dim, float qks, void* stream);
 
+/* qattn_int8_attn_fwd_ex (f16 P.V: vdq = the f16 image of qattn_int8_quant) on a schedule
+ * software-pipelined by two key tiles (csrc/int8_attn_fwd_f2.hip): the softmax of tile t runs beside
+ * the MFMAs of QK^T(t+1) and P.V(t-1).  Non-causal; head_dim 64 / 128; bit-identical to the f16 P.V
+ * mode with the biased S accumulator.  Returns 1 for causal-only or unsupported shapes. */
+int qattn_int8_attn_fwd_f2(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
+                           const void* vdq, void* out, void* lse, long bh, long sq_tok, long sk_tok,
+                           int group, int head_dim, float qks, void* stream);
+
 /* Key-split (flash-decoding) form of qattn_int8_attn_fwd_i8pv_ex, non-causal, for short query blocks
  * against long key ranges (the int8 key/value cache): each workgroup covers
  * keys_per_split keys (multiple of 32) of its query rows and writes the partial softmax state
@@ -164,6 +172,10 @@ int qattn_int8_attn_bwd_ex(const void* dO_i8, const void* sdO, const void* q_i8,
  * ws must hold qattn_int8_bwd_ws_bytes(bh, sq_tok, sk_tok) bytes, 16-byte aligned; it is scratch
  * (overwritten, not read before written).  Returns 1 for ws == NULL. */
 long qattn_int8_bwd_ws_bytes(long bh, long sq_tok, long sk_tok);
+/* The largest dS-record workspace the backwards (int8 and bf16 alike) allocate before they fall back
+ * to recomputation: QATTN_BWD_WS_MAX bytes if that is set, else min(16 GiB, half the free device
+ * memory at the call). */
+long qattn_bwd_ws_cap(void);
 int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
                            const void* k_i8, const void* sk, const void* v_i8, const void* sv,
                            const void* LD, const void* q_bf, const void* k_bf, const void* dO_bf,

@@ -34,6 +34,7 @@ SIGNATURES = {
     "qattn_int8_attn_fwd_i8pv_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                  _vp],
     "qattn_int8_attn_fwd_rs": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
+    "qattn_int8_attn_fwd_f2": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_split": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                _vp],
     "qattn_int8_split_combine": [_vp] * 4 + [_c_long, _c_int, _c_int, _vp],
@@ -42,6 +43,7 @@ SIGNATURES = {
     "qattn_int8_attn_bwd_ws": [_vp] * 16 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                              _c_float, _vp],
     "qattn_int8_bwd_ws_bytes": [_c_long, _c_long, _c_long],
+    "qattn_bwd_ws_cap": [],
     "qattn_int8_attn_bwd_wsc": [_vp] * 16 + [_c_long, _c_long, _c_long, _c_long, _c_int, _c_int, _c_int,
                                               _c_float, _c_float, _vp],
     "qattn_int8_bwd_dkdv_ws": [_vp] * 14 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
@@ -92,7 +94,8 @@ DEV_SIGNATURES = {
 }
 
 # return types other than the int status code
-RESTYPES = {"qattn_int8_bwd_ws_bytes": ctypes.c_long, "qattn_bf16_bwd_ws_bytes": ctypes.c_long}
+RESTYPES = {"qattn_int8_bwd_ws_bytes": ctypes.c_long, "qattn_bf16_bwd_ws_bytes": ctypes.c_long,
+            "qattn_bwd_ws_cap": ctypes.c_long}
 
 _lib = None
 _dev = None

@@ -120,7 +120,8 @@ def helion_flash_atten_2_algo_4_bwd(
     ws = None
     if entry == "ws":
         ws_bytes = _lib.load().qattn_bf16_bwd_ws_bytes(B * H, S, Sk)
-        if 0 < ws_bytes <= WS_MAX_BYTES:
+        cap = _lib.load().qattn_bwd_ws_cap() if WS_MAX_BYTES is None else WS_MAX_BYTES
+        if 0 < ws_bytes <= cap:
             try:
                 ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
             except torch.cuda.OutOfMemoryError:
@@ -138,7 +139,8 @@ def helion_flash_atten_2_algo_4_bwd(
 # the dQ pass saves, causal it is 7 % faster; "qattn_bf16_bwd_split_ex": separate dV
 # and dK kernels.  All give bit-identical gradients.  QATTN_BF16_BWD_WS=1 / 0 forces ws on / off.
 _BWD_ENTRY = {"1": "ws", "0": "qattn_bf16_bwd_ex"}.get(os.environ.get("QATTN_BF16_BWD_WS", ""), "auto")
-WS_MAX_BYTES = int(os.environ.get("QATTN_BWD_WS_MAX", 16 << 30))
+# None: the library's shared cap (qattn_bwd_ws_cap), as the int8 backward and the C++ operators
+WS_MAX_BYTES = None
 
 
 class FlashAttention_2_BF16_autograd_function(Function):

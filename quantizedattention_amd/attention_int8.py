@@ -64,9 +64,11 @@ def _check_shapes(q, k, v):
 #         dequantisation per 32-key tile;
 #   "f16": v_mfma_f32_32x32x16_f16 on f16(P_i8 * sp) x f16(v_i8 * sv), the tile scale in the operands;
 #   "rs": the f16 contraction in the role-split kernel (one MFMA wave and two softmax waves per SIMD)
-#         where it applies (non-causal, head_dim 128), "i8" elsewhere.
+#         where it applies (non-causal, head_dim 128), "i8" elsewhere;
+#   "f2": the f16 contraction software-pipelined by two key tiles (csrc/int8_attn_fwd_f2.hip) where
+#         it applies (non-causal), "f16" elsewhere.
 # Same P_i8, scales and tolerance in every mode; QATTN_INT8_PV selects the default.
-PV_MODES = ("i8", "f16", "rs")
+PV_MODES = ("i8", "f16", "rs", "f2")
 PV_MODE = os.environ.get("QATTN_INT8_PV", "i8")
 
 
@@ -90,6 +92,8 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     Hkv, Sk = k.shape[1], k.shape[2]
     if pv == "rs" and (causal or D != 128):
         pv = "i8"
+    if pv == "f2" and causal:
+        pv = "f16"
     N = B * H * S
     Nkv = B * Hkv * Sk
     dev = q.device
@@ -122,6 +126,11 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
                   D, st)
         _lib.call("qattn_int8_attn_fwd_rs", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
                   _lib.ptr(vop), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, D, qks, st)
+    elif pv == "f2":
+        _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), None,
+                  Nkv, Sk, D, st)
+        _lib.call("qattn_int8_attn_fwd_f2", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
+                  _lib.ptr(vop), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, D, qks, st)
     elif pv == "f16":
         _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), None,
                   Nkv, Sk, D, st)
@@ -142,7 +151,9 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
 # Largest dS workspace (bytes) the backward allocates to skip the dQ pass's recomputation of S,
 # dP, P and dS (qattn_int8_attn_bwd_ws); larger problems recompute (qattn_int8_attn_bwd_ex).  The
 # results are bit-identical either way.  1 B per score + 4 B per 32x32 tile: 2.2 GB at (4,32,4096).
-WS_MAX_BYTES = int(os.environ.get("QATTN_BWD_WS_MAX", 64 << 30))
+# None: the library's shared cap (qattn_bwd_ws_cap: QATTN_BWD_WS_MAX, else min(16 GiB, half the free
+# device memory)), the same rule as the bf16 backward and the C++ operators.
+WS_MAX_BYTES = None
 # Key/value heads per chunk of the record backward (qattn_int8_attn_bwd_wsc): dK+dV then dQ per
 # chunk, one chunk-sized workspace re-used by every chunk; 0: one pass over all heads; unset: auto
 # (non-causal: chunks of >= 512 dK+dV workgroups, two per CU, measured 2-4 % faster than one pass
@@ -220,7 +231,8 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
     # the records of one key/value head (its H / Hkv query heads) are addressed with 32-bit offsets
     region_ok = (H // Hkv) * (S // 32) * (Sk // 32) * 1024 < (1 << 31)
     if use_ws is None:
-        use_ws = 0 <= ws_bytes <= WS_MAX_BYTES and region_ok
+        cap = _lib.load().qattn_bwd_ws_cap() if WS_MAX_BYTES is None else WS_MAX_BYTES
+        use_ws = 0 <= ws_bytes <= cap and region_ok
     elif use_ws and not (region_ok and ws_bytes >= 0):
         raise _lib.QAttnError("qattn int8 backward: dS workspace region exceeds 2 GiB per key/value "
                               "head; use the recomputing backward (use_ws=False)")

@@ -28,6 +28,7 @@
 // each (q-tile, k-tile) dS tile with the same operation order, so tile scales and dS_i8 agree bit
 // for bit.  Tile-wide maxima use DPP + permlane reductions.  No atomics: deterministic.
 #include <climits>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -998,6 +999,17 @@ extern "C" int qattn_int8_bwd_dq(const void* dO_i8, const void* sdO, const void*
 // buffer offsets: that region, G * (sq/32) * (sk/32) KiB, must stay below 2^31 bytes.
 static bool ws_region_fits(long group, long sq_tok, long sk_tok) {
   return group * (sq_tok / 32) * (sk_tok / 32) * 1024 < (1L << 31);
+}
+
+// Largest dS-record workspace either backward (int8 or bf16) allocates before it falls back to
+// recomputation: QATTN_BWD_WS_MAX bytes if set, else min(16 GiB, half the device memory free now).
+extern "C" long qattn_bwd_ws_cap(void) {
+  const char* s = getenv("QATTN_BWD_WS_MAX");
+  if (s != nullptr && *s != 0) return strtol(s, nullptr, 10);
+  long cap = 16L << 30;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && (long)(free_b / 2) < cap) cap = (long)(free_b / 2);
+  return cap;
 }
 
 extern "C" long qattn_int8_bwd_ws_bytes(long bh, long sq_tok, long sk_tok) {

@@ -12,7 +12,7 @@
 //
 // Schemas (reference file:line of the computation each replaces):
 //   int8_quant(Tensor x, int block) -> (Tensor, Tensor)                 attention_int8.py:178-186
-//   int8_fwd(Tensor q, Tensor k, Tensor v, bool smooth, bool causal)    attention_int8.py:20-65, 97-262
+//   int8_fwd(Tensor q, Tensor k, Tensor v, bool smooth, bool causal, str pv)  attention_int8.py:20-65, 97-262
 //       -> (O, lse, q_i8, k_i8, v_i8, sq, sk, sv)        (k_i8 row-major [B*Hkv*Sk, D])
 //   int8_bwd(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, bool causal, int kv_heads)
 //       -> (dq, dk, dv)                                                  attention_int8.py:264-432
@@ -112,8 +112,11 @@ void check_int8(const Tensor& q, const Tensor& k, const Tensor& v) {
 
 using T8 = std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor>;
 
-// attention_int8._int8_forward (P.V on the int8 MFMA unless QATTN_INT8_PV=f16)
-T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smooth, bool causal) {
+// attention_int8._int8_forward.  pv: the P.V mode, as attention_int8.PV_MODES ("i8", "f16", "rs",
+// "f2"; ops.int8_fwd passes attention_int8.PV_MODE); "" = QATTN_INT8_PV, else "i8".  "rs" runs as
+// "i8" where the role-split kernel does not apply (causal, head_dim 64), "f2" as "f16" when causal.
+T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smooth, bool causal,
+            c10::string_view pv_in) {
   check_int8(q_in, k_in, v_in);
   require_gpu({&q_in, &k_in, &v_in});
   Ctx c(q_in);
@@ -121,8 +124,16 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
                v = v_in.to(at::kHalf).contiguous();
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
   const int64_t Hkv = k.size(1), Sk = k.size(2), N = B * H * S, Nkv = B * Hkv * Sk;
-  const char* pv = std::getenv("QATTN_INT8_PV");
-  const bool f16pv = pv && std::string(pv) == "f16";
+  std::string pv(pv_in.data(), pv_in.size());
+  if (pv.empty()) {
+    const char* e = std::getenv("QATTN_INT8_PV");
+    pv = (e && *e) ? e : "i8";
+  }
+  TORCH_CHECK_VALUE(pv == "i8" || pv == "f16" || pv == "rs" || pv == "f2", "qattn int8: unknown P.V mode '",
+                    pv, "' (one of i8, f16, rs, f2)");
+  if (pv == "rs" && (causal || D != 128)) pv = "i8";
+  if (pv == "f2" && causal) pv = "f16";
+  const bool f16pv = pv != "i8";
   Tensor q_i8 = empty({N, D}, at::kChar, q), k_i8 = empty({Nkv, D}, at::kChar, q),
          v_i8 = empty({Nkv, D}, at::kChar, q);
   Tensor sq = empty({N / 32}, at::kHalf, q), sk = empty({Nkv / 32}, at::kHalf, q),
@@ -145,7 +156,18 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
                             c.stream),
        "quantise k");
   const float qks = qk_scale(D);
-  if (f16pv) {
+  if (pv == "rs") {
+    call(qattn_int8_quant_vop(P(v), P(v_i8), P(sv), P(vop), Nkv, (int)D, c.stream), "quantise v");
+    call(qattn_int8_attn_fwd_rs(P(q_i8), P(sq), P(k_i8), P(sk), P(vop), P(O), P(lse), B * H, S, Sk,
+                                (int)(H / Hkv), (int)D, qks, c.stream),
+         "int8 forward");
+  } else if (pv == "f2") {
+    call(qattn_int8_quant(P(v), P(v_i8), P(sv), P(vop), nullptr, Nkv, (int)Sk, (int)D, c.stream),
+         "quantise v");
+    call(qattn_int8_attn_fwd_f2(P(q_i8), P(sq), P(k_i8), P(sk), P(vop), P(O), P(lse), B * H, S, Sk,
+                                (int)(H / Hkv), (int)D, qks, c.stream),
+         "int8 forward");
+  } else if (f16pv) {
     call(qattn_int8_quant(P(v), P(v_i8), P(sv), P(vop), nullptr, Nkv, (int)Sk, (int)D, c.stream),
          "quantise v");
     call(qattn_int8_attn_fwd_ex(P(q_i8), P(sq), P(k_i8), P(sk), P(vop), P(O), P(lse), B * H, S, Sk,
@@ -202,7 +224,7 @@ T3 int8_bwd(const Tensor& dO_in, const Tensor& q_i8_in, const Tensor& sq, const 
   const int64_t ws_bytes = qattn_int8_bwd_ws_bytes(chunk * G, S, Sk);
   const bool region_ok = G * (S / 32) * (Sk / 32) * 1024 < (int64_t(1) << 31);
   Tensor ws;
-  if (ws_bytes > 0 && region_ok && ws_bytes <= env_i64("QATTN_BWD_WS_MAX", int64_t(64) << 30))
+  if (ws_bytes > 0 && region_ok && ws_bytes <= qattn_bwd_ws_cap())
     ws = try_empty(ws_bytes, O);
   if (ws.defined() && chunk < bkv) {
     call(qattn_int8_attn_bwd_wsc(P(dO_i8), P(sdO), P(q_i8), P(sqc), P(k_i8), P(skc), P(v_i8), P(svc),
@@ -281,7 +303,7 @@ T3 bf16_bwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, const Te
   Tensor ws;
   if (want_ws) {
     const int64_t ws_bytes = qattn_bf16_bwd_ws_bytes(B * H, S, Sk);
-    if (ws_bytes > 0 && ws_bytes <= env_i64("QATTN_BWD_WS_MAX", int64_t(16) << 30)) ws = try_empty(ws_bytes, q);
+    if (ws_bytes > 0 && ws_bytes <= qattn_bwd_ws_cap()) ws = try_empty(ws_bytes, q);
   }
   if (ws.defined())
     call(qattn_bf16_bwd_ws_ex(P(q), P(k), P(v), P(dO_bf), P(LD), P(q_bf), P(k_bf), P(dq), P(dk), P(dv),
@@ -381,7 +403,7 @@ Tensor mxfp4_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in) {
 
 TORCH_LIBRARY(qattn, m) {
   m.def("int8_quant(Tensor x, int block) -> (Tensor, Tensor)");
-  m.def("int8_fwd(Tensor q, Tensor k, Tensor v, bool smooth, bool causal) -> "
+  m.def("int8_fwd(Tensor q, Tensor k, Tensor v, bool smooth, bool causal, str pv=\"\") -> "
         "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("int8_bwd(Tensor dO, Tensor q_i8, Tensor sq, Tensor k_i8, Tensor sk, Tensor v_i8, Tensor sv, "
         "Tensor O, Tensor lse, bool causal, int kv_heads) -> (Tensor, Tensor, Tensor)");

@@ -219,7 +219,8 @@ def _pv_mode(pv):
     pv = attention_int8.PV_MODE if pv is None else pv
     if pv not in attention_int8.PV_MODES:
         raise _lib.QAttnError(f"qattn kv cache: unknown P.V mode {pv!r} (one of {attention_int8.PV_MODES})")
-    return "i8" if pv == "rs" else pv
+    # the training-shape schedules run as their contraction's cache path
+    return {"rs": "i8", "f2": "f16"}.get(pv, pv)
 
 
 def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False, pv=None):
@@ -229,7 +230,7 @@ def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False
     are the LAST Sq positions (query i keeps keys <= Sk - Sq + i), Sq <= Sk.  Returns (O fp16
     [B, Hq, Sq, D], lse fp16 [B*Hq*Sq]); without ``causal`` identical to the forward on the un-cached
     tensors (bit-identical when one key split covers the cache).  ``pv``: the P.V mode (default
-    attention_int8.PV_MODE; "rs" runs as "i8" here).
+    attention_int8.PV_MODE; "rs" runs as "i8" and "f2" as "f16" here).
     Non-causal with the int8 P.V at head_dim 128 runs in the decoding layout (_decode_split: the
     grouped query heads of a key/value head in one workgroup, long caches split over the keys and
     merged); the results equal the one-pass forward's up to the merge's rounding (<= 2e-3).

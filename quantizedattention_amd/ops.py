@@ -8,7 +8,7 @@ its fake (meta) implementation, for graph capture (``torch.compile``, ``torch.ex
 the autograd rules of ``int8_fwd`` and ``bf16_fwd`` (their backward operators).
 
     torch.ops.qattn.int8_quant(x, block) -> (idx, scale)
-    torch.ops.qattn.int8_fwd(q, k, v, smooth, causal) -> (O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
+    torch.ops.qattn.int8_fwd(q, k, v, smooth, causal, pv="") -> (O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
     torch.ops.qattn.int8_bwd(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, causal, kv_heads)
         -> (dq, dk, dv)
     torch.ops.qattn.bf16_fwd(q, k, v, causal) -> (O, lse)
@@ -42,7 +42,7 @@ def _(x, block):
 
 
 @torch.library.register_fake("qattn::int8_fwd")
-def _(q, k, v, smooth, causal):
+def _(q, k, v, smooth, causal, pv=""):
     B, H, S, D = q.shape
     Nq, Nkv = B * H * S, k.shape[0] * k.shape[1] * k.shape[2]
     e = lambda *s, dt: q.new_empty(s, dtype=dt)  # noqa: E731
@@ -88,7 +88,8 @@ def _(q, k, v):
 
 # ---------------------------------------------------------------------------- autograd rules
 def _int8_setup(ctx, inputs, output):
-    q, k, v, smooth, causal = inputs
+    q, k, v, smooth, causal = inputs[:5]
+    ctx.n_inputs = len(inputs)
     O, lse, q_i8, k_i8, v_i8, sq, sk, sv = output
     ctx.save_for_backward(O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
     ctx.causal, ctx.kv_heads = causal, k.shape[1]
@@ -100,16 +101,17 @@ def _int8_backward_rule(ctx, dO, *_unused):
     # gradient of O only (the quantised outputs are not differentiable, int8:52-56); k smoothing
     # adds no gradient (softmax-invariant), so the same backward serves smooth and plain forwards
     O, lse, q_i8, k_i8, v_i8, sq, sk, sv = ctx.saved_tensors
+    rest = (None,) * (ctx.n_inputs - 3)   # smooth, causal, pv
     if dO is None:
-        return None, None, None, None, None
+        return (None, None, None) + rest
     qd, kd, vd = ctx.dtypes
     if O.numel() == 0 or k_i8.numel() == 0:   # nothing attends (an empty batch): zero gradients
         z = dict(device=O.device)
         return (torch.zeros(O.shape, dtype=qd, **z), torch.zeros(ctx.kv_shape, dtype=kd, **z),
-                torch.zeros(ctx.kv_shape, dtype=vd, **z), None, None)
+                torch.zeros(ctx.kv_shape, dtype=vd, **z)) + rest
     dq, dk, dv = _ops.int8_bwd(dO.to(torch.float16), q_i8, sq, k_i8, sk, v_i8, sv, O, lse, ctx.causal,
                                ctx.kv_heads)
-    return dq.to(qd), dk.to(kd), dv.to(vd), None, None
+    return (dq.to(qd), dk.to(kd), dv.to(vd)) + rest
 
 
 torch.library.register_autograd("qattn::int8_fwd", _int8_backward_rule, setup_context=_int8_setup)
@@ -140,9 +142,12 @@ def int8_quant(x, block):
     return _ops.int8_quant(x, block)
 
 
-def int8_fwd(q, k, v, smooth, causal):
-    """SageAttention-3 int8 forward (attention_int8.py:97-262, per (batch, head))."""
-    return _ops.int8_fwd(q, k, v, smooth, causal)
+def int8_fwd(q, k, v, smooth, causal, pv=None):
+    """SageAttention-3 int8 forward (attention_int8.py:97-262, per (batch, head)).  ``pv``: the P.V
+    mode (attention_int8.PV_MODES), default attention_int8.PV_MODE -- the drop-ins' mode, so the
+    operator and ``sage_attention_3_int8`` run the same kernel."""
+    from . import attention_int8
+    return _ops.int8_fwd(q, k, v, smooth, causal, attention_int8.PV_MODE if pv is None else pv)
 
 
 def int8_bwd(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, causal, kv_heads):

@@ -24,7 +24,7 @@ def header_decls():
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
     for m in re.finditer(r"\b(int|long)\s+(qattn_\w+)\s*\(([^)]*)\)\s*;", text):
-        params = [p.strip() for p in m.group(3).split(",") if p.strip()]
+        params = [p.strip() for p in m.group(3).split(",") if p.strip() and p.strip() != "void"]
         decls[m.group(2)] = params
     return decls
 

@@ -61,6 +61,12 @@ if entry("qattn_int8_attn_fwd_ex") is not None:
 if entry("qattn_int8_attn_fwd_i8pv_ex") is not None:
     fns["i8"] = lambda: call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv),
                              P(O), P(lse), B * H, S, S, 1, int(causal), D, qks, st)
+if entry("qattn_int8_attn_fwd_f2") is not None and not causal:
+    fns["f2"] = lambda: call("qattn_int8_attn_fwd_f2", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse),
+                             B * H, S, S, 1, D, qks, st)
+only = os.environ.get("QATTN_AB_MODES")
+if only:
+    fns = {k_: f_ for k_, f_ in fns.items() if k_ in only.split(",")}
 ops = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
 name = os.path.basename(path)
 for mode, f in fns.items():

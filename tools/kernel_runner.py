@@ -1,6 +1,6 @@
 """Launch one kernel of the int8 / bf16 paths N times at the headline shape (for rocprofv3 passes).
 
-    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd (f16 P.V), int8_fwd_i8 (default), int8_fwd_rs (role split), int8_dkdv, int8_dv, int8_dk, int8_dq, int8_all, bf16_fwd,
+    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd (f16 P.V), int8_fwd_i8 (default), int8_fwd_rs (role split), int8_fwd_f2 (two-tile pipeline), int8_dkdv, int8_dv, int8_dk, int8_dq, int8_all, bf16_fwd,
                                                            bf16_bwd, jvp, quant
 """
 import math
@@ -57,6 +57,9 @@ for name in [n for _ in range(reps) for n in names]:
     elif name == "int8_fwd_i8":
         _lib.call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv), P(O), P(lse),
                   B * H, S, S, 1, 0, D, qks, st)
+    elif name == "int8_fwd_f2":
+        _lib.call("qattn_int8_attn_fwd_f2", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse), B * H, S, S, 1, D,
+                  qks, st)
     elif name == "int8_fwd_rs":
         _lib.call("qattn_int8_attn_fwd_rs", P(qi), P(sq), P(ki), P(sk), P(vop), P(O), P(lse), B * H, S, S, 1, D,
                   qks, st)
