@@ -145,3 +145,22 @@ def test_jvp_primal_only_bit_identical(lib, dtype, shape):
     torch.cuda.synchronize()
     assert none is None
     assert torch.equal(O, Op) and torch.equal(lse, lsep)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_jvp_non_contiguous_inputs(lib, dtype):
+    """q/k/v and tangents made by transposing [B,S,H,D] tensors (non-contiguous): every contiguous
+    copy must outlive the launch that reads it.  Bit-identical to the call on contiguous copies, for
+    the tangent kernel and the primal-only kernel."""
+    from quantizedattention_amd.attention_jvp import _jvp
+    g = torch.Generator().manual_seed(17)
+    B, S, H, D = 2, 192, 3, 64
+    xs = [torch.randn((B, S, H, D), generator=g).to(dtype).cuda().transpose(1, 2) for _ in range(6)]
+    assert not any(x.is_contiguous() for x in xs)
+    ys = [x.contiguous() for x in xs]
+    O, tO, lse = _jvp(*xs[:3], tuple(xs[3:]))
+    Oc, tOc, lsec = _jvp(*ys[:3], tuple(ys[3:]))
+    Op, _, lsep = _jvp(*xs[:3], None)
+    torch.cuda.synchronize()
+    assert torch.equal(O, Oc) and torch.equal(tO, tOc) and torch.equal(lse, lsec)
+    assert torch.equal(Op, Oc) and torch.equal(lsep, lsec)
