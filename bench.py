@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--skip-bf16", action="store_true")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the other-config timings (a profiled run whose kernels are all config 3)")
     return p.parse_args()
 
 
@@ -108,6 +110,12 @@ def event_time(fn, n):
     return a.elapsed_time(b) / n
 
 
+def ws_chunk_heads(bh, S):
+    """Heads per launch of the step's chunked record backward (attention_int8._ws_chunk)."""
+    from quantizedattention_amd.attention_int8 import _ws_chunk
+    return _ws_chunk(None, False, bh, S)
+
+
 def int8_kernel_times(q, k, v, dO, n):
     """Per-kernel average durations (ms) of the int8 path, each launched alone on the stream."""
     B, H, S, D = q.shape
@@ -127,6 +135,7 @@ def int8_kernel_times(q, k, v, dO, n):
     qb, kb, ob = (e(N, D, dt=torch.bfloat16) for _ in range(3))
     dq, dk, dv = (e(B, H, S, D, dt=torch.float16) for _ in range(3))
     ws = e(_lib.load().qattn_int8_bwd_ws_bytes(B * H, S, S), dt=torch.uint8)
+    chunk = ws_chunk_heads(B * H, S)
     qks, sms = _f32(1 / math.sqrt(D) * 1.44269504), _f32(1 / math.sqrt(D))
     calls = {
         "kmean_kernel": lambda: _lib.call("qattn_kmean", P(k), P(km), B * H, S, D, st),
@@ -160,12 +169,19 @@ def int8_kernel_times(q, k, v, dO, n):
         "int8_bwd_dq_kernel": lambda: _lib.call("qattn_int8_bwd_dq", P(dOi), P(sdO), P(qi), P(sq),
                                                 P(ki), P(sk), P(vi), P(sv), P(LD), P(kb), P(dq),
                                                 B * H, S, D, qks, sms, st),
-        # the step's backward (qattn_int8_attn_bwd_ws): dK+dV writing the dS workspace, dQ from it
+        # the step's backward (qattn_int8_attn_bwd_wsc): per chunk of `chunk` heads, dK+dV writing
+        # the dS workspace, then dQ from it -- timed as the step launches them (one chunk-sized launch)
         "int8_bwd_dkdv_kernel<dK+dV, dS out>": lambda: _lib.call(
             "qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
-            P(qb), P(ob), P(dk), P(dv), P(ws), B * H, S, D, qks, sms, st),
+            P(qb), P(ob), P(dk), P(dv), P(ws), chunk, S, D, qks, sms, st),
         "int8_bwd_dqw_kernel": lambda: _lib.call("qattn_int8_bwd_dq_ws", P(kb), P(sk), P(dq), P(ws),
-                                                 B * H, S, D, sms, st),
+                                                 chunk, S, D, sms, st),
+        # the same two kernels over all B*H heads in one launch each (qattn_int8_attn_bwd_ws)
+        "int8_bwd_dkdv_kernel<dK+dV, dS out, one pass>": lambda: _lib.call(
+            "qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
+            P(qb), P(ob), P(dk), P(dv), P(ws), B * H, S, D, qks, sms, st),
+        "int8_bwd_dqw_kernel<one pass>": lambda: _lib.call("qattn_int8_bwd_dq_ws", P(kb), P(sk), P(dq),
+                                                           P(ws), B * H, S, D, sms, st),
     }
     order = list(calls)
     for name in order:  # populate every buffer once in dependency order
@@ -453,12 +469,15 @@ def main():
             dist.destroy_process_group()
         return
     kt = int8_kernel_times(q, k, v, dO, max(3, a.steps // 2))
+    chunk = ws_chunk_heads(B * H, S)
+    launches = {"int8_attn_fwd_kernel": 1, "int8_bwd_dkdv_kernel<dK+dV, dS out>": -(-B * H // chunk),
+                "int8_bwd_dqw_kernel": -(-B * H // chunk)}   # launches per step
     per_call = {  # algorithmic MFMA work per launch, the step's kernels
         "int8_attn_fwd_kernel": 4.0 * B * H * S * S * D,   # QK^T, PV
-        "int8_bwd_dkdv_kernel<dK+dV, dS out>": 8.0 * B * H * S * S * D,   # S, dP, dV, dK
-        "int8_bwd_dqw_kernel": 2.0 * B * H * S * S * D,    # dQ (S, dP, dS come from the workspace)
+        "int8_bwd_dkdv_kernel<dK+dV, dS out>": 8.0 * chunk * S * S * D,   # S, dP, dV, dK
+        "int8_bwd_dqw_kernel": 2.0 * chunk * S * S * D,    # dQ (S, dP, dS come from the workspace)
     }
-    dom = max(per_call, key=lambda n: kt[n])
+    dom = max(per_call, key=lambda n: kt[n] * launches[n])   # most device time per step
     achieved = per_call[dom] / (kt[dom] * 1e-3) / 1e12
     # the inference forward as a caller sees it: sage_attention_3_int8 without autograd
     # (k-mean + q/k/v quantisation + attention, no bf16 images), one HIP-event-timed call
@@ -494,9 +513,12 @@ def main():
                          fwd_flop / (kt["int8_attn_fwd_kernel"] * 1e-3) / PEAK_I8},
         "kernel_ms": kt,
         "mxfp4_fwd": mxfp4_fwd_times(q, k, v, max(3, a.steps // 2)) if extras and D == 128 else None,
-        "configs": other_configs(max(3, a.steps // 2)) if extras else None,
+        "configs": other_configs(max(3, a.steps // 2)) if extras and not a.no_configs else None,
         "roofline": {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": PEAK_I8 / 1e12,
-                     "unit": "TFLOP/s", "frac": achieved * 1e12 / PEAK_I8, "traffic": None},
+                     "unit": "TFLOP/s", "frac": achieved * 1e12 / PEAK_I8, "traffic": None,
+                     "launch_ms": kt[dom], "work_per_launch": per_call[dom],
+                     "launches_per_step": launches[dom],
+                     "heads_per_launch": B * H if dom == "int8_attn_fwd_kernel" else chunk},
     }
     # HBM bytes per launch from the committed PMC passes (tools/profile_round.sh), only when they
     # were measured on these exact kernel sources and this shape

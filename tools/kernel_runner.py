@@ -17,7 +17,8 @@ from quantizedattention_amd.attention_jvp import helion_attention_jvp_forward_fp
 
 name = sys.argv[1]
 if name == "int8_all":  # every int8 attention kernel once per rep, in step order
-    names = ["int8_fwd_i8", "int8_fwd", "int8_dkdv_ws", "int8_dqw", "int8_dkdv", "int8_dq"]
+    names = ["int8_fwd_i8", "int8_fwd", "int8_dkdv_wsc", "int8_dqw_c", "int8_dkdv_ws", "int8_dqw",
+             "int8_dkdv", "int8_dq"]
 else:
     names = [name]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
@@ -48,6 +49,8 @@ for a_, b_ in ((qi, qb), (ki, kb), (dOi, ob)):
 dq, dk, dv = (torch.empty_like(q) for _ in range(3))
 ws = torch.empty((_lib.load().qattn_int8_bwd_ws_bytes(B * H, S, S),), dtype=torch.uint8, device="cuda")
 vb = v.bfloat16()
+from quantizedattention_amd.attention_int8 import _ws_chunk  # noqa: E402
+CHUNK = _ws_chunk(None, False, B * H, S)   # heads per launch of the step's record backward
 if name.startswith("bf16"):
     Ob, lseb = helion_atten_bf16_fwd_training(q, k, vb, False)
 torch.cuda.synchronize()
@@ -72,6 +75,11 @@ for name in [n for _ in range(reps) for n in names]:
     elif name == "int8_dkdv_ws":
         _lib.call("qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv),
                   P(LD), P(qb), P(ob), P(dk), P(dv), P(ws), B * H, S, D, qks, sms, st)
+    elif name == "int8_dkdv_wsc":   # one launch of the step's chunked record backward (CHUNK heads)
+        _lib.call("qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv),
+                  P(LD), P(qb), P(ob), P(dk), P(dv), P(ws), CHUNK, S, D, qks, sms, st)
+    elif name == "int8_dqw_c":
+        _lib.call("qattn_int8_bwd_dq_ws", P(kb), P(sk), P(dq), P(ws), CHUNK, S, D, sms, st)
     elif name == "int8_dqw":
         _lib.call("qattn_int8_bwd_dq_ws", P(kb), P(sk), P(dq), P(ws), B * H, S, D, sms, st)
     elif name == "int8_dq":

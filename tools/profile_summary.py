@@ -1,6 +1,6 @@
 """Turn a tools/profile_round.sh output directory into the committed profile artefacts.
 
-    python tools/profile_summary.py gpurun_out/prof_<tag> <tag>
+    python tools/profile_summary.py gpurun_out/prof_<tag> <tag> [out dir, default profiles/]
 
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats of the bench command (verbatim)
@@ -14,21 +14,29 @@ import glob
 import json
 import os
 import re
-import shutil
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
 
-# bench.py kernel keys -> normalised rocprof kernel-name patterns (D = 128 instantiations)
+# bench.py kernel keys -> (normalised rocprof kernel-name pattern, workgroups per launch or None) of
+# the D = 128 instantiations at config 3 (4,32,4096,128).  The record backward runs in chunks of
+# CHUNK heads (attention_int8._ws_chunk: 32 at config 3), so its kernels appear with two grids: the
+# chunk launch the step runs, and the one-pass launch over all 128 heads.
+BH, S = 4 * 32, 4096
+CHUNK = 32
 KEYS = {
-    "int8_attn_fwd_kernel": r"int8_attn_fwd_kernel(<128, ?1, ?false>|ILi128ELi1ELb0E)",
-    "int8_attn_fwd_kernel<f16 P.V>": r"int8_attn_fwd_kernel(<128, ?0, ?false>|ILi128ELi0ELb0E)",
-    "int8_bwd_dkdv_kernel<dK+dV>": r"int8_bwd_kernel(<128, ?3, ?false, ?false>|ILi128ELi3ELb0ELb0E)",
-    "int8_bwd_dq_kernel": r"int8_bwd_kernel(<128, ?2|ILi128ELi2E)",
-    "int8_bwd_dkdv_kernel<dK+dV, dS out>": r"int8_bwd_kernel(<128, ?3, ?false, ?true>|ILi128ELi3ELb0ELb1E)",
-    "int8_bwd_dqw_kernel": r"int8_bwd_dqw_kernel(<128|ILi128E)",
+    "int8_attn_fwd_kernel": (r"int8_attn_fwd_kernel(<128, ?1, ?false>|ILi128ELi1ELb0E)", None),
+    "int8_attn_fwd_kernel<f16 P.V>": (r"int8_attn_fwd_kernel(<128, ?0, ?false>|ILi128ELi0ELb0E)", None),
+    "int8_bwd_dkdv_kernel<dK+dV>": (r"int8_bwd_kernel(<128, ?3, ?false, ?false>|ILi128ELi3ELb0ELb0E)", None),
+    "int8_bwd_dq_kernel": (r"int8_bwd_kernel(<128, ?2|ILi128ELi2E)", None),
+    "int8_bwd_dkdv_kernel<dK+dV, dS out>": (r"int8_bwd_kernel(<128, ?3, ?false, ?true>|ILi128ELi3ELb0ELb1E)",
+                                            CHUNK * S // 256),
+    "int8_bwd_dkdv_kernel<dK+dV, dS out, one pass>": (
+        r"int8_bwd_kernel(<128, ?3, ?false, ?true>|ILi128ELi3ELb0ELb1E)", BH * S // 256),
+    "int8_bwd_dqw_kernel": (r"int8_bwd_dqw_kernel(<128|ILi128E)", CHUNK * S // 256),
+    "int8_bwd_dqw_kernel<one pass>": (r"int8_bwd_dqw_kernel(<128|ILi128E)", BH * S // 256),
 }
 SIMDS_PER_XCD = 32 * 4
 # GRBM_GUI_ACTIVE is summed over the 8 XCDs; SQ_VALU_MFMA_BUSY_CYCLES counts 32 busy SIMD-cycles per
@@ -40,10 +48,20 @@ def norm(name):
     return re.sub(r"\s+", "", name)
 
 
-def key_of(name):
+def workgroups(row):
+    """Workgroups of a dispatch from a rocprofv3 CSV row (Grid_Size / Workgroup_Size, in work-items)."""
+    try:
+        g = int(float(row.get("Grid_Size") or row.get("Grid_Size_X") or 0))
+        w = int(float(row.get("Workgroup_Size") or row.get("Workgroup_Size_X") or 0))
+        return g // w if w else None
+    except ValueError:
+        return None
+
+
+def key_of(name, wgs=None):
     n = norm(name)
-    for k, pat in KEYS.items():
-        if re.search(pat, n):
+    for k, (pat, want) in KEYS.items():
+        if re.search(pat, n) and (want is None or wgs is None or want == wgs):
             return k
     return None
 
@@ -54,7 +72,7 @@ def counters(d):
     kinds = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            k = key_of(row["Kernel_Name"])
+            k = key_of(row["Kernel_Name"], workgroups(row))
             if k is None:
                 continue
             per[(k, row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
@@ -67,16 +85,8 @@ def counters(d):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    os.makedirs(PROF, exist_ok=True)
-    stats = glob.glob(os.path.join(src, "bench", "**", "*kernel_stats.csv"), recursive=True)
-    if stats:
-        shutil.copy(stats[0], os.path.join(PROF, f"{tag}_kernel_stats.csv"))
-    bj = os.path.join(src, "bench.json")
-    if os.path.exists(bj):
-        lines = [ln for ln in open(bj) if ln.startswith("{")]
-        if lines:
-            with open(os.path.join(PROF, f"{tag}_bench.json"), "w") as f:
-                f.write(lines[-1])
+    out_dir = sys.argv[3] if len(sys.argv) > 3 else PROF
+    os.makedirs(out_dir, exist_ok=True)
     fetch = counters(os.path.join(src, "fetch"))
     write = counters(os.path.join(src, "write"))
     mfma = counters(os.path.join(src, "mfma"))
@@ -105,13 +115,13 @@ def main():
             traffic[k] = e["FETCH_bytes_x2"] + e["WRITE_bytes"]
             e["hbm_bytes_per_launch"] = traffic[k]
         out[k] = e
-    with open(os.path.join(PROF, f"{tag}_pmc.json"), "w") as f:
+    with open(os.path.join(out_dir, f"{tag}_pmc.json"), "w") as f:
         json.dump({"note": "FETCH_SIZE/WRITE_SIZE are KB per dispatch from rocprofv3; FETCH doubled "
                            "per MI355X_MICROARCH.md (gfx950 reports half of wide streaming reads)",
                    "kernels": out}, f, indent=1)
     sys.path.insert(0, ROOT)
     from bench import source_hash
-    with open(os.path.join(PROF, "traffic_latest.json"), "w") as f:
+    with open(os.path.join(out_dir, "traffic_latest.json"), "w") as f:
         # bench.py reports these only while the kernel sources hash to source_sha256
         json.dump({"tag": tag, "source_sha256": source_hash(), "shape": [4, 32, 4096, 128],
                    "traffic": traffic}, f, indent=1)
