@@ -28,6 +28,7 @@
 // each (q-tile, k-tile) dS tile with the same operation order, so tile scales and dS_i8 agree bit
 // for bit.  Tile-wide maxima use DPP + permlane reductions.  No atomics: deterministic.
 #include <climits>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.h"
@@ -170,6 +171,9 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #define QA_DKV_STAGGER 1
 #endif
 // cache policy of the dS record stores (builtin aux: 2 = nt, 16 = sc1)
+#ifndef QA_BWD_PACK_ASM
+#define QA_BWD_PACK_ASM 1
+#endif
 
 
 template <int D, int ROLE>
@@ -249,6 +253,62 @@ struct BwdDma {
     if constexpr (G::HAS_LD) dma4_buf(ld_rsrc, 4 * lane, (unsigned)t * 256, slot_lds + G::LDO);
   }
 };
+
+// Inline-asm VALU blocks here write only registers tied to their inputs ("+v"): hipcc's hazard
+// recogniser does not look inside inline asm, and an asm output placed in a register that an
+// in-flight MFMA still reads as its A/B operand is overwritten too early (an untied version of the
+// record packing below corrupted dq).  A tied register holds a VALU result that no
+// MFMA reads, or a copy the compiler made (its own hazard waits included).
+
+// y = RTZ_f32(x * inv + 2^23) = 2^23 + floor(x * inv) for 0 <= x * inv < 2^23 (the f32 spacing is 1
+// in [2^23, 2^24)): the truncation of a non-negative quantiser step folded into its multiply, in
+// place (y = x on entry).  MODE.FP_ROUND[1:0] (f32) = 3 (toward zero) only around the 16 ops (an
+// s_setreg builtin does not order the compiler's FP ops against it).  floor of the exact product:
+// differs from trunc(RNE(x * inv)) only when the product lies within half an ulp below an integer.
+QA_DEVICE void floor_magic16(float* y, float inv) {
+  const float magic = 8388608.0f;
+  asm("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 2), 3\n\t"
+      "s_nop 1\n\t"
+      "v_fma_f32 %0, %0, %16, %17\n\tv_fma_f32 %1, %1, %16, %17\n\t"
+      "v_fma_f32 %2, %2, %16, %17\n\tv_fma_f32 %3, %3, %16, %17\n\t"
+      "v_fma_f32 %4, %4, %16, %17\n\tv_fma_f32 %5, %5, %16, %17\n\t"
+      "v_fma_f32 %6, %6, %16, %17\n\tv_fma_f32 %7, %7, %16, %17\n\t"
+      "v_fma_f32 %8, %8, %16, %17\n\tv_fma_f32 %9, %9, %16, %17\n\t"
+      "v_fma_f32 %10, %10, %16, %17\n\tv_fma_f32 %11, %11, %16, %17\n\t"
+      "v_fma_f32 %12, %12, %16, %17\n\tv_fma_f32 %13, %13, %16, %17\n\t"
+      "v_fma_f32 %14, %14, %16, %17\n\tv_fma_f32 %15, %15, %16, %17\n\t"
+      "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 2), 0\n\t"
+      "s_nop 1"
+      : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]),
+        "+v"(y[7]), "+v"(y[8]), "+v"(y[9]), "+v"(y[10]), "+v"(y[11]), "+v"(y[12]), "+v"(y[13]),
+        "+v"(y[14]), "+v"(y[15])
+      : "v"(inv), "s"(magic));
+}
+
+// The int8 bytes of 16 integer-valued floats in [-127, 127], packed low to high (byte j of the
+// result = x[j]): each conversion writes its byte in place (SDWA dst_sel), 16 instructions instead
+// of 16 conversions and 12 byte permutes (tools/ubench/sdwa_probe.hip checks the byte placement).
+// Dword w is built in the register of x[4w] (tied, see above).  The four dwords are built
+// interleaved, byte b of every dword before byte b + 1: back to back, a partial (PRESERVE) write
+// read a stale register and lost byte 2 (measured: tools/ws_records.py).
+QA_DEVICE v4i pack16_i8(const float* x) {
+  float r0 = x[0], r1 = x[4], r2 = x[8], r3 = x[12];
+#define QA_SDWA(R, A, B, U) \
+  "v_cvt_i32_f32_sdwa " R ", " A " dst_sel:BYTE_" B " dst_unused:UNUSED_" U " src0_sel:DWORD\n\t"
+  asm(QA_SDWA("%0", "%0", "0", "PAD") QA_SDWA("%1", "%1", "0", "PAD")
+      QA_SDWA("%2", "%2", "0", "PAD") QA_SDWA("%3", "%3", "0", "PAD")
+      QA_SDWA("%0", "%4", "1", "PRESERVE") QA_SDWA("%1", "%7", "1", "PRESERVE")
+      QA_SDWA("%2", "%10", "1", "PRESERVE") QA_SDWA("%3", "%13", "1", "PRESERVE")
+      QA_SDWA("%0", "%5", "2", "PRESERVE") QA_SDWA("%1", "%8", "2", "PRESERVE")
+      QA_SDWA("%2", "%11", "2", "PRESERVE") QA_SDWA("%3", "%14", "2", "PRESERVE")
+      QA_SDWA("%0", "%6", "3", "PRESERVE") QA_SDWA("%1", "%9", "3", "PRESERVE")
+      QA_SDWA("%2", "%12", "3", "PRESERVE") QA_SDWA("%3", "%15", "3", "PRESERVE")
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3)
+      : "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[9]), "v"(x[10]),
+        "v"(x[11]), "v"(x[13]), "v"(x[14]), "v"(x[15]));
+#undef QA_SDWA
+  return v4i{__float_as_int(r0), __float_as_int(r1), __float_as_int(r2), __float_as_int(r3)};
+}
 
 // max over |x| of 16 values (v_max3_f32 with abs modifiers)
 QA_DEVICE float max16_abs3(const float* x) {
@@ -365,12 +425,15 @@ void int8_bwd_kernel(
       if constexpr (TWO) pa = mfma_i8(*reinterpret_cast<const v4i*>(base + G::Y8B + roff[s]), xb[s], pa);
     }
   };
-  // fp32 P and/or dS of tile t
-  auto values = [&](int t, const v16i& sa, const v16i& pa, float* P, float* dS) {
+  // fp32 P and/or dS of tile t.  maskc (std::true_type / false_type): whether the causal mask is
+  // compiled in -- false_type for tiles past the workgroup's diagonal band, where no score is masked
+  // (the same values: the mask changes nothing there)
+  auto values = [&](int t, const v16i& sa, const v16i& pa, float* P, float* dS, auto maskc) {
+    constexpr bool MASK = CAUSAL && decltype(maskc)::value;
     // causal: position of the tile's first streamed row; the mask is applied only on tiles that
     // cross this wave's diagonal (the streamed side is queries for dK/dV, keys for dQ)
     const int y0 = (32 * t) % Smod;
-    const bool diag = CAUSAL && (ROLE == ROLE_DQ ? (y0 + 31 > x0) : (x0 + 31 > y0));
+    const bool diag = MASK && (ROLE == ROLE_DQ ? (y0 + 31 > x0) : (x0 + 31 > y0));
     // c1 = sq*(sk*qks), c2 = sdO*sv with the streamed / own roles of each kernel
     const float sy_a = (float)sc_lds[t], sy_b = (float)sc_lds[nt + t];
     float c1, c2;
@@ -397,7 +460,7 @@ void int8_bwd_kernel(
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
           float p = exp2_f32(fmaf((float)sa[i], c1, -lse_r[j]));
-          if (CAUSAL && dd > 8 * g + j) p = 0.f;   // key > query: x0 + c32 > y0 + 8g + 4h + j
+          if (MASK && dd > 8 * g + j) p = 0.f;   // key > query: x0 + c32 > y0 + 8g + 4h + j
           if constexpr (G::WANT_P) P[i] = p;
           if constexpr (G::WANT_DS) dS[i] = p * fmaf((float)pa[i], c2, -d_r[j]);
         }
@@ -409,7 +472,7 @@ void int8_bwd_kernel(
       for (int i = 0; i < 16; ++i) {
         float p = exp2_f32(fmaf((float)sa[i], c1, -lsex));
         // key > query: y0 + (i & 3) + 8 (i >> 2) + 4h > x0 + c32
-        if (CAUSAL && dd > -((i & 3) + 8 * (i >> 2))) p = 0.f;
+        if (MASK && dd > -((i & 3) + 8 * (i >> 2))) p = 0.f;
         dS[i] = p * fmaf((float)pa[i], c2, -Dx);
       }
     }
@@ -424,6 +487,33 @@ void int8_bwd_kernel(
   };
   auto quantise = [&](const float* X, float so, v8bf* op) {
     quantise_m(X, so, op, wave_max_nonneg(max16_abs3(X)));
+  };
+  // the P operand (P >= 0): trunc = floor, folded into the multiply (floor_magic16), and
+  // q * c = fma(2^23 + q, c, -2^23 c) exactly (2^23 c is exact): 2 ops per value instead of 3
+  auto quantise_p = [&](const float* X, float so, v8bf* op, float xmax) {
+    const float sx = xmax * (1.0f / 127.0f);
+    const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
+    const float c = sx * so;
+    const float nc = -8388608.0f * c;
+    float y[16];
+#if QA_BWD_PACK_ASM
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y[i] = X[i];
+    floor_magic16(y, inv);
+#else
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y[i] = __builtin_truncf(X[i] * inv) + 8388608.0f;
+#endif
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      v4u w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i0 = 8 * s + 2 * j;
+        w[j] = pk_bf16(fmaf(y[i0], c, nc), fmaf(y[i0 + 1], c, nc));
+      }
+      op[s] = __builtin_bit_cast(v8bf, w);
+    }
   };
   auto tr_load = [&](int t, int region, v8bf* ta) {
     const char* base = slot(t) + region;
@@ -474,6 +564,9 @@ void int8_bwd_kernel(
         for (int j = 0; j < 4; ++j) w[j] = pk_bf16(q[8 * s + 2 * j] * c, q[8 * s + 2 * j + 1] * c);
         op[s] = __builtin_bit_cast(v8bf, w);
       }
+#if QA_BWD_PACK_ASM
+      const v4i bytes = pack16_i8(q);
+#else
       v4i bytes;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -483,6 +576,7 @@ void int8_bwd_kernel(
                                                   0x0c0c0400u);
         bytes[d] = (int)__builtin_amdgcn_perm(hi, lo, 0x05040100u);
       }
+#endif
       // record of (query head bh*G + t/nqt, q-tile t%nqt, key tile x0/32), relative to this key/value
       // head's first record (ws_rsrc / sc_rsrc): SGPR offsets, no per-lane address arithmetic
       const int nqt = Smod / 32, nkt = Sx / 32;
@@ -503,7 +597,7 @@ void int8_bwd_kernel(
     if (active && t0 < nt) {
       v16i sa, pa;
       products(t0, sa, pa);
-      values(t0, sa, pa, X, X);
+      values(t0, sa, pa, X, X, std::true_type{});
     }
     for (int t = t0; t < nt; ++t) {
       // tile t+1 landed (later tiles may be in flight); the slot of tile t-1 is free
@@ -517,78 +611,93 @@ void int8_bwd_kernel(
         v16i sa, pa;
         products(tn, sa, pa);
         v8bf op[2];
-        quantise(X, ROLE == ROLE_DV ? so_p(t) : so_ds(t), op);
+        if constexpr (ROLE == ROLE_DV) quantise_p(X, so_p(t), op, wave_max_nonneg(max16_abs3(X)));
+        else quantise(X, so_ds(t), op);
         accumulate(acc, ta, op);
-        values(tn, sa, pa, X, X);
-      }
-    }
-  } else if (QA_DKV_PIPE || (QA_DKV_STAGGER && wave >= G::WAVES / 2)) {
-    // DKV pipelined: carry the quantised bf16 operands of tile t (16 VGPRs) into iteration t, whose
-    // int8 products for tile t+1 are issued first and whose fp32 values of t+1 are computed beside
-    // the bf16 MFMAs of tile t
-    v8bf opS[2], opP[2];
-    if (active && t0 < nt) {
-      v16i sa, pa;
-      products(t0, sa, pa);
-      float P[16], dS[16];
-      values(t0, sa, pa, P, dS);
-      float mS = max16_abs3(dS), mP = max16_abs3(P);
-      wave_max2_nonneg(mS, mP);   // (the two tile maxima in one interleaved reduction)
-      quantise_ds(dS, t0, opS, mS);
-      quantise_m(P, so_p(t0), opP, mP);
-    }
-    for (int t = t0; t < nt; ++t) {
-      // tile t+1 landed: younger than its DMA are the workspace stores of tile t-1, the DMA of
-      // tile t+2 and the stores of tile t
-      if (active) ring_wait_barrier<(G::NSLOT - 3) * G::IPW + 2 * WS_OPS>();
-      else ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
-      dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
-                min(t + G::NSLOT - 1, nt - 1), lane);
-      if (active) {
-        const int tn = min(t + 1, nt - 1);
-        v16i sa, pa;
-        products(tn, sa, pa);
-        v8bf ta[2 * C::NDB];
-        tr_load(t, G::TR, ta);
-        accumulate(acc, ta, opS);          // dK += q^T dS
-        tr_load(t, G::TR2, ta);
-        accumulate(acc2, ta, opP);         // dV += dO^T P
-        float P[16], dS[16];
-        values(tn, sa, pa, P, dS);
-        float mS = max16_abs3(dS), mP = max16_abs3(P);
-        wave_max2_nonneg(mS, mP);   // (the two tile maxima in one interleaved reduction)
-        quantise_ds(dS, tn, opS, mS);
-        quantise_m(P, so_p(tn), opP, mP);
+        values(tn, sa, pa, X, X, std::true_type{});
       }
     }
   } else {
-    for (int t = t0; t < nt; ++t) {
-      // tile t landed (t+1, t+2 may be in flight); the slot of tile t-1 is free.  With the stagger
-      // the other half of the workgroup reads tile t+1 after this barrier: wait for it too.
-      // (the workspace stores of an active wave, WS_OPS per tile, sit between the DMAs)
-      if (active)
-        ring_wait_barrier<(G::NSLOT - (QA_DKV_STAGGER ? 3 : 2)) * G::IPW +
-                          (QA_DKV_STAGGER ? 2 : 3) * WS_OPS>();
-      else
-        ring_wait_barrier<(G::NSLOT - (QA_DKV_STAGGER ? 3 : 2)) * G::IPW>();
-      dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
-                min(t + G::NSLOT - 1, nt - 1), lane);
-      if (active) {
+    // Fused dK+dV.  Causal without grouped heads (the streamed rows are one query head): the tiles
+    // t0 .. t0 + WAVES - 1 hold every wave's diagonal; past this band no score of the workgroup is
+    // masked, and those tiles run with the mask compiled out (bit-identical, ~36 fewer vector
+    // instructions per tile-wave).  Grouped heads stream the group's query heads one after another,
+    // so their diagonals recur: masked throughout.
+    const int tb = !CAUSAL ? t0 : (Ny == Smod ? min(nt, t0 + G::WAVES) : nt);
+    if (QA_DKV_PIPE || (QA_DKV_STAGGER && wave >= G::WAVES / 2)) {
+      // DKV pipelined: carry the quantised bf16 operands of tile t (16 VGPRs) into iteration t, whose
+      // int8 products for tile t+1 are issued first and whose fp32 values of t+1 are computed beside
+      // the bf16 MFMAs of tile t
+      v8bf opS[2], opP[2];
+      if (active && t0 < nt) {
         v16i sa, pa;
-        products(t, sa, pa);
+        products(t0, sa, pa);
         float P[16], dS[16];
-        values(t, sa, pa, P, dS);
-        v8bf opS[2], opP[2];
+        values(t0, sa, pa, P, dS, std::true_type{});
         float mS = max16_abs3(dS), mP = max16_abs3(P);
         wave_max2_nonneg(mS, mP);   // (the two tile maxima in one interleaved reduction)
-        quantise_ds(dS, t, opS, mS);
-        quantise_m(P, so_p(t), opP, mP);
-        v8bf ta[2 * C::NDB];
-        tr_load(t, G::TR, ta);
-        accumulate(acc, ta, opS);          // dK += q^T dS
-        tr_load(t, G::TR2, ta);
-        accumulate(acc2, ta, opP);         // dV += dO^T P
+        quantise_ds(dS, t0, opS, mS);
+        quantise_p(P, so_p(t0), opP, mP);
       }
+      auto iter = [&](int t, auto maskc) {
+        // tile t+1 landed: younger than its DMA are the workspace stores of tile t-1, the DMA of
+        // tile t+2 and the stores of tile t
+        if (active) ring_wait_barrier<(G::NSLOT - 3) * G::IPW + 2 * WS_OPS>();
+        else ring_wait_barrier<(G::NSLOT - 3) * G::IPW>();
+        dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
+                  min(t + G::NSLOT - 1, nt - 1), lane);
+        if (active) {
+          const int tn = min(t + 1, nt - 1);
+          v16i sa, pa;
+          products(tn, sa, pa);
+          v8bf ta[2 * C::NDB];
+          tr_load(t, G::TR, ta);
+          accumulate(acc, ta, opS);          // dK += q^T dS
+          tr_load(t, G::TR2, ta);
+          accumulate(acc2, ta, opP);         // dV += dO^T P
+          float P[16], dS[16];
+          values(tn, sa, pa, P, dS, maskc);  // (tile t+1 of the last band iteration: mask-free anyway)
+          float mS = max16_abs3(dS), mP = max16_abs3(P);
+          wave_max2_nonneg(mS, mP);   // (the two tile maxima in one interleaved reduction)
+          quantise_ds(dS, tn, opS, mS);
+          quantise_p(P, so_p(tn), opP, mP);
+        }
+      };
+      int t = t0;
+      for (; t < tb; ++t) iter(t, std::true_type{});
+      for (; t < nt; ++t) iter(t, std::false_type{});
+    } else {
+      auto iter = [&](int t, auto maskc) {
+        // tile t landed (t+1, t+2 may be in flight); the slot of tile t-1 is free.  With the stagger
+        // the other half of the workgroup reads tile t+1 after this barrier: wait for it too.
+        // (the workspace stores of an active wave, WS_OPS per tile, sit between the DMAs)
+        if (active)
+          ring_wait_barrier<(G::NSLOT - (QA_DKV_STAGGER ? 3 : 2)) * G::IPW +
+                            (QA_DKV_STAGGER ? 2 : 3) * WS_OPS>();
+        else
+          ring_wait_barrier<(G::NSLOT - (QA_DKV_STAGGER ? 3 : 2)) * G::IPW>();
+        dma.issue(smem_lds + ((t + G::NSLOT - 1) % G::NSLOT) * G::SLOT,
+                  min(t + G::NSLOT - 1, nt - 1), lane);
+        if (active) {
+          v16i sa, pa;
+          products(t, sa, pa);
+          float P[16], dS[16];
+          values(t, sa, pa, P, dS, maskc);
+          v8bf opS[2], opP[2];
+          float mS = max16_abs3(dS), mP = max16_abs3(P);
+          wave_max2_nonneg(mS, mP);   // (the two tile maxima in one interleaved reduction)
+          quantise_ds(dS, t, opS, mS);
+          quantise_p(P, so_p(t), opP, mP);
+          v8bf ta[2 * C::NDB];
+          tr_load(t, G::TR, ta);
+          accumulate(acc, ta, opS);          // dK += q^T dS
+          tr_load(t, G::TR2, ta);
+          accumulate(acc2, ta, opP);         // dV += dO^T P
+        }
+      };
+      int t = t0;
+      for (; t < tb; ++t) iter(t, std::true_type{});
+      for (; t < nt; ++t) iter(t, std::false_type{});
     }
   }
   vmcnt_wait_all();
