@@ -1,79 +1,71 @@
-"""Instruction mix of a kernel's main loop from hipcc assembly (dev tool).
+"""Instruction mix of a kernel's loops from hipcc assembly (dev tool).
 
-    python tools/isa_loop.py <file.s> [kernel-substring]
+    hipcc -O3 --offload-arch=gfx950 --cuda-device-only -S <src.hip> -o <file.s> (+ the build flags)
+    python tools/isa_loop.py <file.s> <kernel symbol or unique substring> [first last]
 
-Prints, per kernel, the basic blocks of the outermost backward-branch loop with their VALU / MFMA
-/ LDS / SALU counts, so an edit's effect on the per-tile issue cost is visible
-without a GPU run."""
+Prints every loop (a backward branch to a label of the kernel) with its VALU / transcendental /
+packed-fp32 / MFMA / LDS / VMEM / SALU / s_nop / s_waitcnt counts, so an edit's effect on the
+per-tile issue cost is visible without a GPU run; with [first last] (instruction
+indices printed for a loop) also the per-opcode histogram of that range."""
+import collections
 import re
 import sys
 
 
-def blocks(body):
-    cur, out = "entry", {}
-    order = []
-    for ln in body.split("\n"):
-        t = ln.strip()
-        m = re.match(r"^(\.LBB[\w_]+):", t) or re.match(r"^; (%bb\.\d+):", t)
-        if m:
-            cur = m.group(1)
-            order.append(cur)
-            out[cur] = []
-            continue
-        if not t or t.startswith((";", ".")):
-            continue
-        out.setdefault(cur, []).append(t.split(";")[0].strip())
-        if cur not in order:
-            order.append(cur)
-    return order, out
-
-
 def kind(i):
-    if i.startswith("v_mfma"):
+    op = i.split()[0]
+    if op.startswith("v_mfma"):
         return "mfma"
-    if i.startswith(("v_exp", "v_log", "v_rcp", "v_sqrt", "v_rsq")):
+    if op.startswith(("v_exp", "v_log", "v_rcp", "v_sqrt", "v_rsq")):
         return "trans"
-    if i.startswith("v_"):
+    if op.startswith("v_pk_") and "f32" in op:
+        return "pkf32"
+    if op.startswith("v_"):
         return "valu"
-    if i.startswith("ds_"):
+    if op.startswith("ds_"):
         return "lds"
-    if i.startswith(("buffer_", "global_")):
+    if op.startswith(("buffer_", "global_")):
         return "vmem"
-    if i.startswith("s_"):
+    if op.startswith("s_nop"):
+        return "nop"
+    if op.startswith("s_waitcnt"):
+        return "wait"
+    if op.startswith("s_"):
         return "salu"
     return "other"
 
 
 def main():
-    s = open(sys.argv[1]).read()
-    sel = sys.argv[2] if len(sys.argv) > 2 else ""
-    for m in re.finditer(r"\n(_Z\w+):[^\n]*\n(.*?)\.Lfunc_end", s, re.S):
-        name, body = m.group(1), m.group(2)
-        if sel not in name:
+    src = open(sys.argv[1]).read()
+    names = [m.group(1) for m in re.finditer(r"^([\w.$]+):", src, re.M) if sys.argv[2] in m.group(1)
+             and not m.group(1).startswith(".")]
+    if not names:
+        sys.exit(f"no kernel matching {sys.argv[2]!r}")
+    kname = names[0]
+    start = src.index("\n" + kname + ":")
+    end = src.index(".Lfunc_end", start)
+    labels, insts = {}, []
+    for ln in src[start:end].split("\n")[1:]:
+        t = ln.strip()
+        m = re.match(r"^(\.LBB[\w_]+):", t)
+        if m:
+            labels[m.group(1)] = len(insts)
             continue
-        order, bl = blocks(body)
-        idx = {b: i for i, b in enumerate(order)}
-        loop = None
-        for b in order:
-            for ins in bl[b]:
-                mm = re.match(r"s_(?:cbranch_\w+|branch)\s+(\.LBB[\w_]+)", ins)
-                if mm and mm.group(1) in idx and idx[mm.group(1)] <= idx[b]:
-                    span = (idx[mm.group(1)], idx[b])
-                    if loop is None or span[1] - span[0] > loop[1] - loop[0]:
-                        loop = span
-        print(name)
-        if loop is None:
-            print("  no loop")
+        if not t or t.startswith((";", ".")) or t.endswith(":"):
             continue
-        tot = {}
-        for b in order[loop[0]:loop[1] + 1]:
-            c = {}
-            for ins in bl[b]:
-                k = kind(ins)
-                c[k] = c.get(k, 0) + 1
-                tot[k] = tot.get(k, 0) + 1
-            print(f"  {b:24s} " + " ".join(f"{k}={v}" for k, v in sorted(c.items())))
-        print("  loop total: " + " ".join(f"{k}={v}" for k, v in sorted(tot.items())))
+        insts.append(t.split(";")[0].strip())
+    print(kname)
+    for idx, i in enumerate(insts):
+        m = re.match(r"s_(cbranch_\w+|branch)\s+(\.LBB[\w_]+)", i)
+        if m and labels.get(m.group(2), 1 << 30) <= idx:
+            a = labels[m.group(2)]
+            c = collections.Counter(kind(x) for x in insts[a:idx + 1])
+            print(f"  loop {m.group(2)} [{a}..{idx}] n={idx + 1 - a}: "
+                  + " ".join(f"{k}={v}" for k, v in sorted(c.items())))
+    if len(sys.argv) > 4:
+        a, b = int(sys.argv[3]), int(sys.argv[4])
+        for k, v in collections.Counter(x.split()[0] for x in insts[a:b + 1]).most_common():
+            print(f"{v:5d} {k}")
 
 
 if __name__ == "__main__":
