@@ -170,6 +170,13 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #ifndef QA_DKV_STAGGER
 #define QA_DKV_STAGGER 1
 #endif
+// fused dK+dV workgroup shape (A/B builds): waves (32 keys each) and LDS ring slots
+#ifndef QA_DKV_WAVES
+#define QA_DKV_WAVES 8
+#endif
+#ifndef QA_DKV_NSLOT
+#define QA_DKV_NSLOT 4
+#endif
 // cache policy of the dS record stores (builtin aux: 2 = nt, 16 = sc1)
 #ifndef QA_BWD_PACK_ASM
 #define QA_BWD_PACK_ASM 1
@@ -184,7 +191,7 @@ struct BwdCfg {
   static constexpr bool WANT_P = ROLE == ROLE_DV || ROLE == ROLE_DKV;
   static constexpr bool WANT_DS = ROLE != ROLE_DV;
   static constexpr int NTR = (ROLE == ROLE_DKV) ? 2 : 1;    // transposed images per tile
-  static constexpr int WAVES = (ROLE == ROLE_DKV) ? 8 : 4;
+  static constexpr int WAVES = (ROLE == ROLE_DKV) ? QA_DKV_WAVES : 4;
   static constexpr bool PIPE = ROLE != ROLE_DKV;
   static constexpr int Y8A = 0;
   static constexpr int Y8B = C::T8;
@@ -192,7 +199,7 @@ struct BwdCfg {
   static constexpr int TR2 = TR + C::T16;                   // DKV: dO image (P product)
   static constexpr int LDO = TR + NTR * C::T16;
   static constexpr int SLOT = LDO + (HAS_LD ? 256 : 0);
-  static constexpr int NSLOT = 4;
+  static constexpr int NSLOT = (ROLE == ROLE_DKV) ? QA_DKV_NSLOT : 4;
   static constexpr int NP8 = C::T8 / 1024, NP16 = C::T16 / 1024;
   static constexpr int INST = NP8 * (TWO ? 2 : 1) + NTR * NP16;   // 1-KiB pieces per tile
   static constexpr int IPW16 = (INST + WAVES - 1) / WAVES;
