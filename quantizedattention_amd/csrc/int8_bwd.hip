@@ -170,6 +170,9 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #ifndef QA_DKV_STAGGER
 #define QA_DKV_STAGGER 1
 #endif
+#ifndef QA_DKV_I8DV_COST
+#define QA_DKV_I8DV_COST 0
+#endif
 // fused dK+dV workgroup shape (A/B builds): waves (32 keys each) and LDS ring slots
 #ifndef QA_DKV_WAVES
 #define QA_DKV_WAVES 8
@@ -532,6 +535,22 @@ void int8_bwd_kernel(
         ta[s * C::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * 2 * D));
       }
   };
+  // Timing-only cost model (A/B builds, -DQA_DKV_I8DV_COST=1; results are wrong): dV on the int8
+  // MFMA as the reference's hl.dot(P_i8^T, dO_i8) (int8:375-378) -- 4 v_mfma_i32_32x32x32_i8 from a
+  // biased seed and the per-tile dequantisation of the 64 accumulator elements per lane -- in place
+  // of the 8 bf16 MFMAs of the folded-scale operand; operands are stand-ins of the same registers.
+  auto accumulate_i8cost = [&](v16f* ac, const v8bf* ta, const v8bf* op, float c) {
+    v16i seed;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) seed[i] = KMAG_BITS;
+    // one d block at a time (a 64-register int32 product beside the fp32 accumulators spills)
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) {
+      const v16i pacc = mfma_i8(__builtin_bit_cast(v4i, ta[b]), __builtin_bit_cast(v4i, op[0]), seed);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ac[b][r] = fmaf(__int_as_float(pacc[r]), c, ac[b][r]);
+    }
+  };
   auto accumulate = [&](v16f* ac, const v8bf* ta, const v8bf* op) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -661,7 +680,11 @@ void int8_bwd_kernel(
           tr_load(t, G::TR, ta);
           accumulate(acc, ta, opS);          // dK += q^T dS
           tr_load(t, G::TR2, ta);
+#if QA_DKV_I8DV_COST
+          accumulate_i8cost(acc2, ta, opP, so_p(t));
+#else
           accumulate(acc2, ta, opP);         // dV += dO^T P
+#endif
           float P[16], dS[16];
           values(tn, sa, pa, P, dS, maskc);  // (tile t+1 of the last band iteration: mask-free anyway)
           float mS = max16_abs3(dS), mP = max16_abs3(P);
@@ -699,7 +722,11 @@ void int8_bwd_kernel(
           tr_load(t, G::TR, ta);
           accumulate(acc, ta, opS);          // dK += q^T dS
           tr_load(t, G::TR2, ta);
+#if QA_DKV_I8DV_COST
+          accumulate_i8cost(acc2, ta, opP, so_p(t));
+#else
           accumulate(acc2, ta, opP);         // dV += dO^T P
+#endif
         }
       };
       int t = t0;
