@@ -36,6 +36,10 @@ int qattn_probe_fp4_cvt(const void* x, const void* s, void* packed, void* back, 
  * (s bits, x bits, reference index, index, image bits). */
 int qattn_probe_quant_div(int s_lo, int s_hi, void* bad, void* stream);
 
+/* Device copy of `bytes` (a multiple of 16) by exactly `workgroups` workgroups of 256 threads
+ * (grid-stride): an RCCL-like few-workgroup copy for the overlap probe (tools/overlap_probe.py). */
+int qattn_probe_few_wg_copy(const void* src, void* dst, long bytes, int workgroups, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

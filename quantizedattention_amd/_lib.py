@@ -91,6 +91,7 @@ DEV_SIGNATURES = {
     "qattn_probe_fp4_cvt": [_vp] * 5,
     "qattn_probe_fwd_helpers": [_vp] * 7,
     "qattn_probe_quant_div": [_c_int, _c_int, _vp, _vp],
+    "qattn_probe_few_wg_copy": [_vp, _vp, _c_long, _c_int, _vp],
 }
 
 # return types other than the int status code

@@ -205,3 +205,19 @@ extern "C" int qattn_probe_quant_div(int s_lo, int s_hi, void* bad, void* stream
                      s_lo, s_hi, (unsigned*)bad);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// A device copy by a FIXED number of workgroups (grid-stride, 16 B per lane and step): a stand-in for
+// an RCCL collective kernel, which moves its bytes with a few persistent workgroups (one per
+// channel), next to a grid-filling copy (tools/overlap_probe.py).
+__global__ __launch_bounds__(256) void few_wg_copy_kernel(const uint4* __restrict__ src,
+                                                          uint4* __restrict__ dst, long n16) {
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+}
+extern "C" int qattn_probe_few_wg_copy(const void* src, void* dst, long bytes, int workgroups,
+                                       void* stream) {
+  if (bytes % 16 != 0 || workgroups < 1) return 1;
+  hipLaunchKernelGGL(few_wg_copy_kernel, dim3((unsigned)workgroups), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)src, (uint4*)dst, bytes / 16);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

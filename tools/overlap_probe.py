@@ -1,5 +1,8 @@
 """Does a CU-based copy overlap the int8 backward?  (Proxy for RCCL's CU kernels during dK+dV at
-config 4, SURVEY §8e: each rank receives 470 MB of O.)  Dev tool:  python tools/overlap_probe.py
+config 4, SURVEY §8e: each rank receives 470 MB of O.)  Dev tool:
+    python tools/overlap_probe.py [chunks] [add | memcpy | few<N>]
+add: a grid-filling elementwise kernel; memcpy: hipMemcpyAsync D2D; few<N>: a copy kernel of exactly
+N workgroups (as an RCCL collective moves its bytes with a few persistent workgroups).
 
 Times, HIP events on the compute stream: the config-3 int8 backward alone; a 470 MB device copy
 (an elementwise CU kernel, out = src + 0) alone on a side stream; both launched together.  If the
@@ -11,6 +14,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+from quantizedattention_amd import _lib  # noqa: E402
 from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward  # noqa: E402
 
 torch.cuda.init()
@@ -37,6 +41,10 @@ def copy():
     for c in range(chunks):
         if MODE == "add":      # an elementwise CU kernel
             torch.add(src[c * step:(c + 1) * step], 0, out=dst[c * step:(c + 1) * step])
+        elif MODE.startswith("few"):   # a copy kernel of a fixed, small number of workgroups
+            a, b = src[c * step:(c + 1) * step], dst[c * step:(c + 1) * step]
+            _lib.call("qattn_probe_few_wg_copy", _lib.ptr(a), _lib.ptr(b), a.numel() * 2,
+                      int(MODE[3:]), _lib.stream_of(b))
         else:                  # hipMemcpyAsync device-to-device (the runtime picks blit kernel or SDMA)
             dst[c * step:(c + 1) * step].copy_(src[c * step:(c + 1) * step])
 
