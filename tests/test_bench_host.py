@@ -57,3 +57,41 @@ def test_cpu_info_and_threads():
 def test_source_hash_tracks_the_kernel_sources():
     h = bench.source_hash()
     assert len(h) == 64 and h == bench.source_hash()
+
+
+def test_chunk_heads_match_the_step():
+    """bench.py times the record backward as the step launches it: chunks of >= 512 dK+dV
+    workgroups (attention_int8._ws_chunk), 32 heads at config 3 -> 4 launches per step."""
+    assert bench.ws_chunk_heads(128, 4096) == 32
+    assert bench.ws_chunk_heads(4, 256) == 4        # small problems: one launch over all heads
+
+
+def test_profile_tools_tell_grids_apart(tmp_path):
+    """tools/profile_summary.key_of separates the chunk-sized and one-pass launches of the same
+    kernel by their grids, and tools/trace_summary.py groups a kernel trace per (kernel, grid)."""
+    import csv
+    import subprocess
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from profile_summary import key_of, workgroups
+    name = "void qattn::int8_bwd_kernel<128, 3, false, true>(signed char const*)"
+    assert key_of(name, 512) == "int8_bwd_dkdv_kernel<dK+dV, dS out>"
+    assert key_of(name, 2048) == "int8_bwd_dkdv_kernel<dK+dV, dS out, one pass>"
+    assert key_of("void qattn::int8_attn_fwd_kernel<128, 1, false>(x)", 4096) == "int8_attn_fwd_kernel"
+    assert workgroups({"Grid_Size_X": "262144", "Workgroup_Size_X": "512"}) == 512
+    d = tmp_path / "trace"
+    d.mkdir()
+    cols = ["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Grid_Size_X", "Workgroup_Size_X",
+            "LDS_Block_Size"]
+    rows = [(name, 0, 500, 262144, 512, 1024), (name, 1000, 1510, 262144, 512, 1024),
+            (name, 2000, 4000, 1048576, 512, 1024)]
+    with open(d / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(cols)
+        w.writerows(rows)
+    out = tmp_path / "shapes.csv"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_summary.py"), str(d), str(out)],
+                   check=True, capture_output=True)
+    got = {r["bench_key"]: r for r in csv.DictReader(open(out))}
+    assert got["int8_bwd_dkdv_kernel<dK+dV, dS out>"]["Calls"] == "2"
+    assert got["int8_bwd_dkdv_kernel<dK+dV, dS out>"]["AverageNs"] == "505"
+    assert got["int8_bwd_dkdv_kernel<dK+dV, dS out, one pass>"]["AverageNs"] == "2000"
