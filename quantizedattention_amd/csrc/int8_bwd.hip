@@ -264,11 +264,10 @@ struct BwdDma {
   }
 };
 
-// Inline-asm VALU blocks here write only registers tied to their inputs ("+v"): hipcc's hazard
-// recogniser does not look inside inline asm, and an asm output placed in a register that an
-// in-flight MFMA still reads as its A/B operand is overwritten too early (an untied version of the
-// record packing below corrupted dq).  A tied register holds a VALU result that no
-// MFMA reads, or a copy the compiler made (its own hazard waits included).
+// Inline-asm VALU blocks here write only registers tied to their inputs ("+v"), as a precaution:
+// hipcc's hazard recogniser does not look inside inline asm, so an asm output placed in a register
+// an in-flight MFMA still reads would get no wait states.  A tied register holds a VALU result that
+// no MFMA reads, or a copy the compiler made (its own hazard waits included).
 
 // y = RTZ_f32(x * inv + 2^23) = 2^23 + floor(x * inv) for 0 <= x * inv < 2^23 (the f32 spacing is 1
 // in [2^23, 2^24)): the truncation of a non-negative quantiser step folded into its multiply, in
@@ -299,8 +298,9 @@ QA_DEVICE void floor_magic16(float* y, float inv) {
 // result = x[j]): each conversion writes its byte in place (SDWA dst_sel), 16 instructions instead
 // of 16 conversions and 12 byte permutes (tools/ubench/sdwa_probe.hip checks the byte placement).
 // Dword w is built in the register of x[4w] (tied, see above).  The four dwords are built
-// interleaved, byte b of every dword before byte b + 1: back to back, a partial (PRESERVE) write
-// read a stale register and lost byte 2 (measured: tools/ws_records.py).
+// interleaved, byte b of every dword before byte b + 1: back to back, SDWA partial (PRESERVE) writes
+// to one register lose byte 2 (tools/ubench/sdwa_probe.hip: 1012 of 1024 dwords wrong; this
+// corrupted dq, tools/ws_records.py) -- a hazard hipcc would have padded around its own code.
 QA_DEVICE v4i pack16_i8(const float* x) {
   float r0 = x[0], r1 = x[4], r2 = x[8], r3 = x[12];
 #define QA_SDWA(R, A, B, U) \
