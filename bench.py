@@ -434,11 +434,11 @@ def main():
     O_full = torch.empty((world * B * H, S, D), dtype=torch.float16, device=dev) if gather else None
     comm = torch.cuda.Stream(device=dev) if gather else None
 
-    def step_int8():
+    def step_int8(with_gather=True):
         # the autograd path of sage_attention_3_int8: quantiser passes also write the bf16 images
         O, lse, qi, kiT, vi, sq, sk, sv, km, qb_, kb_ = _int8_forward(q, k, v, smooth=True, images=True)
         work = None
-        if gather:
+        if gather and with_gather:
             comm.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(comm):
                 work = dist.all_gather_into_tensor(O_full, O.view(B * H, S, D), async_op=True)
@@ -449,6 +449,8 @@ def main():
 
     flop_fb = 14.0 * B * H * S * S * D     # this rank's work per step
     t_i8 = timed(step_int8, a.steps, a.warmup, world)
+    # N > 1 (SURVEY §8e "with and without the all-gather"): the same step without the O gather
+    t_ng = timed(lambda: step_int8(False), a.steps, a.warmup, world) if gather else None
     extras = world == 1 and not a.skip_bf16
     res_bf = None
     if extras:
@@ -514,6 +516,10 @@ def main():
         "kernel_ms": kt,
         "mxfp4_fwd": mxfp4_fwd_times(q, k, v, max(3, a.steps // 2)) if extras and D == 128 else None,
         "configs": other_configs(max(3, a.steps // 2)) if extras and not a.no_configs else None,
+        "per_gpu": {"TOPS": flop_fb / t_i8 / 1e12, "frac_of_int8_peak": flop_fb / t_i8 / PEAK_I8},
+        "without_gather": None if t_ng is None else {
+            "value": flop_step / t_ng / 1e12, "ms_per_step": t_ng * 1e3,
+            "gather_cost_ms": (t_i8 - t_ng) * 1e3},
         "roofline": {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": PEAK_I8 / 1e12,
                      "unit": "TFLOP/s", "frac": achieved * 1e12 / PEAK_I8, "traffic": None,
                      "launch_ms": kt[dom], "work_per_launch": per_call[dom],
