@@ -775,6 +775,9 @@ void int8_bwd_kernel(
 #ifndef QA_DQW_NT
 #define QA_DQW_NT 1
 #endif
+#ifndef QA_DQW_NSLOT
+#define QA_DQW_NSLOT 4
+#endif
 // The dK+dV kernel (8 waves) writes records only for q-tiles >= its workgroup's first key tile,
 // and this kernel reads every key tile up to its workgroup's last query tile for all of its waves:
 // with more than 8 waves per workgroup the first ones would read records never written (causal).
@@ -783,7 +786,7 @@ template <int D>
 struct DqwCfg {
   static constexpr int WAVES = QA_DQW_WAVES;
   static constexpr int T16 = 64 * D;               // bf16 k image of a 32-key tile (L2-resident)
-  static constexpr int NSLOT = 4;                  // k image ring: 3 tiles ahead
+  static constexpr int NSLOT = QA_DQW_NSLOT;       // k image ring: NSLOT - 1 tiles ahead
 #ifdef QA_DQW_RSLOT
   static constexpr int RSLOT = QA_DQW_RSLOT;
 #else
