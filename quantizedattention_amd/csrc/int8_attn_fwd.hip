@@ -18,7 +18,9 @@
 //     PV(t)     O^T += V^T . P^T                      (PV modes below)
 //     SM1(t+1)  d = S - rowmax, deferred running max  (VALU, beside the PV(t) MFMAs)
 // Reference rounding points (int8:197-257):
-//     S  = f16(acc * c),  c = sq*sk*qks          one v_fma_mix per score on the biased accumulator
+//     S  = f16(acc * c),  c = sq*sk*qks          on the biased accumulator: one v_pk_fma_f32 per pair
+//                                                + v_cvt_pk_f16_f32 (QA_FWD_S_PK, default), or one
+//                                                v_fma_mix per score
 //                                                (common.h KMAG: no int -> float conversion)
 //     rm = f16(max_k(acc) * c)                   (c > 0: the row max commutes with the scaling)
 //     d  = f16(S - rm)                           (S rounded to f16 first, as the reference does)
@@ -223,7 +225,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     // S = f16(X * c) (int8:200-203: fp32 products, then fp16)
     v2h s2[8];
     _Float16 rm;
-    if constexpr (C::QK_BIAS) {   // on the biased accumulator: one v_fma_mix per score
+    if constexpr (C::QK_BIAS) {   // on the biased accumulator (QA_FWD_S_PK: packed f32, else fma_mix)
       const float c = kmag_scale(cq * ck_lds[t]);
       const float nb = -KMAG * c;
 #if QA_FWD_S_PK
