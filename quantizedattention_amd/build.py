@@ -57,7 +57,32 @@ def build(verbose: bool = True, jobs: int = 8) -> Path:
     _build_lib(sorted(CSRC.glob("*.hip")), LIB, "", verbose, jobs)
     _build_lib(sorted((CSRC / "dev").glob("*.hip")), DEV_LIB, "dev_", verbose, jobs)
     build_torch_ops(verbose)
+    build_c_host(verbose)
     return LIB
+
+
+C_HOST_SRC = PKG.parent / "tests" / "c_abi" / "int8_step.cpp"
+C_HOST_BIN = PKG.parent / "tests" / "c_abi" / "int8_step"
+
+
+def build_c_host(verbose: bool = True) -> Path | None:
+    """tests/c_abi/int8_step: a host program of the C ABI alone (no torch, no Python), linked to
+    libqattn.so through the $ORIGIN-relative rpath; tests/test_gpu_c_abi.py runs it."""
+    if not C_HOST_SRC.exists():
+        return None
+    deps = [C_HOST_SRC, LIB] + list(INCLUDE.glob("*.h"))
+    if C_HOST_BIN.exists() and C_HOST_BIN.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
+        return C_HOST_BIN
+    cmd = [HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", f"-I{INCLUDE}", str(C_HOST_SRC),
+           "-o", str(C_HOST_BIN) + ".tmp", f"-L{PKG}", "-lqattn",
+           "-Wl,-rpath,$ORIGIN/../../quantizedattention_amd"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"C host build failed:\n{r.stderr}")
+    os.replace(str(C_HOST_BIN) + ".tmp", C_HOST_BIN)
+    if verbose:
+        print(f"[qattn build] linked {C_HOST_BIN}", file=sys.stderr)
+    return C_HOST_BIN
 
 
 def build_torch_ops(verbose: bool = True) -> Path:
