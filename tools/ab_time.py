@@ -83,5 +83,10 @@ for mode, f in fns.items():
         ts.append(a.elapsed_time(b))
     ts.sort()
     t = ts[len(ts) // 2]
+    if os.environ.get("QATTN_AB_SAVE"):   # O and lse of the last mode timed, for a bitwise diff
+        torch.save({"O": O.cpu(), "lse": lse.cpu()}, os.environ["QATTN_AB_SAVE"])
+    import hashlib
+    digest = hashlib.sha256(O.view(torch.int16).cpu().numpy().tobytes() +
+                            lse.view(torch.int16).cpu().numpy().tobytes()).hexdigest()[:12]
     print(f"{name} pv={mode}{' causal' if causal else ''}: {t * 1e3:.1f} us  {ops / t / 1e9:.0f} TOPS "
-          f"({ops / t / 1e9 / 5033 * 100:.1f}% i8 peak)", flush=True)
+          f"({ops / t / 1e9 / 5033 * 100:.1f}% i8 peak)  O/lse {digest}", flush=True)
