@@ -336,6 +336,22 @@ QA_DEVICE float max16_abs3(const float* x) {
 // 16 bytes per lane, and its scale s_dS) to the dS workspace that int8_bwd_dqw_kernel reads, so the
 // dQ pass does not recompute S, dP, P and dS.  Tile record (query head, q-tile, key tile) =
 // ((bh_q * nqt + qt) * nkt + kt): 1024 bytes in ds8, one float in sds.
+// Diagnostic build only (-DQA_DKV_STAMP=1, tools/dkv_stamps.py): s_memrealtime stamps (100 MHz) of
+// every fused dK+dV workgroup with records -- entry, end of the prologue, end of the tile loop, exit
+// -- written by lane 0 of wave 0 with vector stores to a buffer of their own that no other code reads.
+#ifndef QA_DKV_STAMP
+#define QA_DKV_STAMP 0
+#endif
+#if QA_DKV_STAMP
+__device__ unsigned long long g_dkv_stamp[4096][4];
+#define DKV_STAMP(k)                                                                            \
+  do {                                                                                          \
+    if (ROLE == ROLE_DKV && WS && threadIdx.x == 0 && blockIdx.x < 4096)                         \
+      g_dkv_stamp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                            \
+  } while (0)
+#else
+#define DKV_STAMP(k) do { } while (0)
+#endif
 template <int D, int ROLE, bool CAUSAL = false, bool WS = false>
 __global__ __launch_bounds__((64 * BwdCfg<D, ROLE>::WAVES), (8 / BwdCfg<D, ROLE>::WAVES))
 void int8_bwd_kernel(
@@ -350,6 +366,7 @@ void int8_bwd_kernel(
   using G = BwdCfg<D, ROLE>;
   constexpr bool TWO = G::TWO;
   static_assert(!WS || ROLE == ROLE_DKV, "the dS workspace is written by the fused dK+dV kernel");
+  DKV_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
   int bh, xt;
@@ -618,6 +635,7 @@ void int8_bwd_kernel(
 
   vmem_drain();
   __syncthreads();
+  DKV_STAMP(1);
   if constexpr (G::PIPE) {
     float X[16];
     if (active && t0 < nt) {
@@ -735,6 +753,7 @@ void int8_bwd_kernel(
     }
   }
   vmcnt_wait_all();
+  DKV_STAMP(2);
   if (!active) return;
   if constexpr (WS) {   // this wave's s_dS column: record (t, x0/32) of the key/value head
     const int nkt = Sx / 32;
@@ -755,6 +774,10 @@ void int8_bwd_kernel(
   };
   store(acc, ROLE == ROLE_DV ? 1.0f : sms, out);
   if constexpr (ROLE == ROLE_DKV) store(acc2, 1.0f, out2);
+#if QA_DKV_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  DKV_STAMP(3);
+#endif
 }
 
 
@@ -1211,6 +1234,12 @@ extern "C" int qattn_int8_attn_bwd_wsc(const void* dO_i8, const void* sdO, const
   }
   return 0;
 }
+
+#if QA_DKV_STAMP
+extern "C" int qattn_dkv_stamps(void* host_dst) {
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(qattn::g_dkv_stamp), sizeof(qattn::g_dkv_stamp)) == hipSuccess ? 0 : 2;
+}
+#endif
 
 // The two parts of qattn_int8_attn_bwd_ws, launchable alone (per-kernel timing).
 extern "C" int qattn_int8_bwd_dkdv_ws(const void* dO_i8, const void* sdO, const void* q_i8,

@@ -1,0 +1,62 @@
+"""Where a fused dK+dV workgroup's time goes (dev tool): the diagnostic build -DQA_DKV_STAMP=1
+(tools/ab_build.sh int8_bwd.hip stamp -DQA_DKV_STAMP=1) stamps entry, end of prologue, end of the
+tile loop and exit of every workgroup (s_memrealtime, 100 MHz); this runs one config-3 chunk launch
+(32 heads, 512 workgroups) and prints the phase durations and the dispatch rounds.
+
+    QATTN_AB=_ab/libqattn_stamp.so python tools/dkv_stamps.py [S] [heads]"""
+import ctypes
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from quantizedattention_amd._lib import SIGNATURES  # noqa: E402
+
+torch.cuda.init()
+lib = ctypes.CDLL(os.environ["QATTN_AB"], mode=ctypes.RTLD_GLOBAL)
+fn = lib.qattn_int8_bwd_dkdv_ws
+fn.argtypes = SIGNATURES["qattn_int8_bwd_dkdv_ws"]
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+bh = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+D = 128
+N = bh * S
+g = torch.Generator(device="cuda").manual_seed(0)
+i8 = lambda: torch.randint(-127, 128, (N, D), device="cuda", generator=g, dtype=torch.int8)  # noqa: E731
+sc = lambda: (torch.rand(N // 32, device="cuda", generator=g) * 0.01 + 0.01).half()  # noqa: E731
+qi, ki, vi, dOi = i8(), i8(), i8(), i8()
+sq, sk, sv, sdO = sc(), sc(), sc(), sc()
+qb, ob = qi.bfloat16(), dOi.bfloat16()
+LD = torch.stack([torch.full((N,), 12.0, device="cuda"), torch.zeros(N, device="cuda")], 1).contiguous()
+dk, dv = (torch.empty((N, D), dtype=torch.float16, device="cuda") for _ in range(2))
+wsb = ctypes.CDLL(os.environ["QATTN_AB"]).qattn_int8_bwd_ws_bytes
+wsb.argtypes = [ctypes.c_long] * 3
+wsb.restype = ctypes.c_long
+ws = torch.empty((wsb(bh, S, S),), dtype=torch.uint8, device="cuda")
+P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
+sms = float(torch.tensor(1 / math.sqrt(D), dtype=torch.float32))
+for _ in range(3):
+    rc = fn(P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD), P(qb), P(ob), P(dk), P(dv),
+            P(ws), bh, S, D, qks, sms, st)
+    assert rc == 0
+torch.cuda.synchronize()
+buf = np.zeros((4096, 4), dtype=np.uint64)
+assert lib.qattn_dkv_stamps(ctypes.c_void_p(buf.ctypes.data)) == 0
+nwg = bh * S // 256
+t = buf[:nwg].astype(np.int64)
+t -= t[:, 0].min()
+us = t / 100.0   # 100 MHz ticks -> us
+pro, loop, epi = us[:, 1] - us[:, 0], us[:, 2] - us[:, 1], us[:, 3] - us[:, 2]
+print(f"{nwg} workgroups, kernel span {us[:, 3].max():.1f} us")
+for name, x in (("prologue", pro), ("tile loop", loop), ("epilogue", epi), ("start", us[:, 0]),
+                ("end", us[:, 3])):
+    print(f"  {name:9s} min {x.min():7.1f}  median {np.median(x):7.1f}  max {x.max():7.1f} us")
+order = np.argsort(us[:, 0])
+starts = us[order, 0]
+print("  start-time histogram (us):", np.histogram(starts, bins=8)[0].tolist(),
+      np.round(np.histogram(starts, bins=8)[1], 1).tolist())
