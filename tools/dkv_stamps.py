@@ -40,7 +40,7 @@ P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
 sms = float(torch.tensor(1 / math.sqrt(D), dtype=torch.float32))
-for _ in range(3):
+for _ in range(int(os.environ.get("REPS", "3"))):   # launches before the stamped (last) one
     rc = fn(P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD), P(qb), P(ob), P(dk), P(dv),
             P(ws), bh, S, D, qks, sms, st)
     assert rc == 0
@@ -60,3 +60,11 @@ order = np.argsort(us[:, 0])
 starts = us[order, 0]
 print("  start-time histogram (us):", np.histogram(starts, bins=8)[0].tolist(),
       np.round(np.histogram(starts, bins=8)[1], 1).tolist())
+# loop time by XCD (bid & 7), by key block (the workgroup's xt under xcd_remap) and by round
+bid = np.arange(nwg)
+nxb = S // 256
+xt = (bid >> 3) % nxb
+rnd = (us[:, 0] > us[:, 0].min() + 5).astype(int)
+for name, key, n in (("xcd", bid & 7, 8), ("key block", xt, nxb), ("round", rnd, 2)):
+    med = [np.median(loop[key == i]) if (key == i).any() else float("nan") for i in range(n)]
+    print(f"  loop median by {name}: " + " ".join(f"{m:.1f}" for m in med))
