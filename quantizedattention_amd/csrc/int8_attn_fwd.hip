@@ -82,6 +82,22 @@ struct SmTile {
 // (the causal PV_F16 kernel's diagonal masking does not fit 168 VGPRs: 2 waves per SIMD)
 template <int D, int PV, bool CAUSAL>
 constexpr int fwd_wps() { return CAUSAL ? 2 : Int8FwdCfg<D, PV>::WPS; }
+// Diagnostic build only (-DQA_FWD_STAMP=1, tools/fwd_stamps.py): s_memrealtime stamps (100 MHz) of
+// every workgroup -- entry, end of the prologue, end of the tile loop, exit -- written by lane 0 of
+// wave 0 with vector stores to a buffer of their own that no other code reads.
+#ifndef QA_FWD_STAMP
+#define QA_FWD_STAMP 0
+#endif
+#if QA_FWD_STAMP
+__device__ unsigned long long g_fwd_stamp[8192][4];
+#define FWD_STAMP(k)                                                                            \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < 8192)                                                  \
+      g_fwd_stamp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                            \
+  } while (0)
+#else
+#define FWD_STAMP(k) do { } while (0)
+#endif
 template <int D, int PV, bool CAUSAL, bool SPLIT = false>
 __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CAUSAL>())) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
@@ -90,6 +106,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     float qks) {
   static_assert(!SPLIT || (PV == PV_I8 && !CAUSAL), "key splits: int8 P.V, non-causal");
   using C = Int8FwdCfg<D, PV>;
+  FWD_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per-tile scales: ck = sk * qks (f32); PV_I8 also sv / 127 (f32)
   float* ck_lds = reinterpret_cast<float*>(smem + C::RING);
@@ -385,6 +402,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
 
   vmem_drain();
   __syncthreads();
+  FWD_STAMP(1);
 
   SmTile st;
   if (active) {
@@ -422,6 +440,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   }
   vmcnt_wait_all();
   __syncthreads();   // every wave is done with the ring: its slots become the output staging area
+  FWD_STAMP(2);
 
   if (!active) return;
   if constexpr (SPLIT) {   // the partial state of this key range: {m, l} and f16(O / l)
@@ -440,6 +459,10 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   const float inv = 1.0f / l;
   store_rows<D, _Float16, 1, PV == PV_I8>(o, inv, smem + wave * RowTile<D, _Float16>::BYTES,
                                           out + (head_row0 + q0) * D, lane, -KMAG * obias * inv);
+#if QA_FWD_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  FWD_STAMP(3);
+#endif
 }
 
 template <int D, int PV, bool CAUSAL>
@@ -536,6 +559,12 @@ static int fwd_dispatch(const void* q_i8, const void* sq, const void* k_i8, cons
 }  // namespace qattn
 
 using namespace qattn;
+
+#if QA_FWD_STAMP
+extern "C" int qattn_fwd_stamps(void* host_dst) {
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(qattn::g_fwd_stamp), sizeof(qattn::g_fwd_stamp)) == hipSuccess ? 0 : 2;
+}
+#endif
 
 extern "C" int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const void* k_i8,
                                       const void* sk, const void* vdq, void* out, void* lse, long bh,

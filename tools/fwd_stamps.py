@@ -1,6 +1,12 @@
+"""Where an int8 forward workgroup's time goes (dev tool): the diagnostic build -DQA_FWD_STAMP=1
+(tools/ab_build.sh int8_attn_fwd.hip fstamp -DQA_FWD_STAMP=1) stamps entry, end of prologue, end of
+the tile loop and exit of every workgroup (s_memrealtime, 100 MHz); this runs the config-3 forward
+(REPS launches, stamps of the last) and prints the phase durations.
+
+    QATTN_AB=_ab/libqattn_fstamp.so [REPS=20] python tools/fwd_stamps.py"""
 import ctypes, math, os, sys
 import numpy as np, torch
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from quantizedattention_amd._lib import SIGNATURES
 torch.cuda.init()
 lib = ctypes.CDLL(os.environ["QATTN_AB"], mode=ctypes.RTLD_GLOBAL)
