@@ -90,5 +90,9 @@ int main(int argc, char** argv) {
   write_file(dir + "/dk.f16", dk, f16b);
   write_file(dir + "/dv.f16", dv, f16b);
   std::printf("int8_step ok: %ld x %d, workspace %ld B\n", N, D, ws_bytes);
+  for (void* p : {q, k, v, dO, q_i8, k_i8, v_i8, vt, sq, sk, sv, k_mean, q_bf, k_bf, O, lse, dO_i8, sdO, LD,
+                  dO_bf, dq, dk, dv, ws})
+    CHECK_HIP(hipFree(p));
+  CHECK_HIP(hipStreamDestroy(st));
   return 0;
 }
