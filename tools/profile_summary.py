@@ -5,7 +5,8 @@
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats of the bench command (verbatim)
   profiles/<tag>_bench.json         the bench JSON line printed under the profiler
-  profiles/<tag>_pmc.json           per kernel: FETCH_SIZE (raw and x2-corrected), WRITE_SIZE, MFMA busy
+  profiles/<tag>_pmc.json           per kernel: FETCH_SIZE (raw and x2-corrected), WRITE_SIZE, MFMA busy,
+                                    the effective clock of the profiled dispatch (clock_GHz)
   profiles/traffic_latest.json      bench kernel key -> HBM bytes per launch (FETCH x2 + WRITE), which
                                     bench.py reports as roofline.traffic
 """
@@ -69,17 +70,20 @@ def key_of(name, wgs=None):
 def counters(d):
     """{bench key: {counter: mean per dispatch}} from one --pmc pass directory."""
     per = defaultdict(float)
-    kinds = {}
+    dur = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             k = key_of(row["Kernel_Name"], workgroups(row))
             if k is None:
                 continue
             per[(k, row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
-            kinds[k] = True
+            if row.get("Start_Timestamp") and row.get("End_Timestamp"):
+                dur[(k, row["Dispatch_Id"])] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
     acc = defaultdict(lambda: defaultdict(list))
     for (k, _, c), v in per.items():
         acc[k][c].append(v)
+    for (k, _), v in dur.items():   # the profiled dispatch's duration (ns)
+        acc[k]["dispatch_ns"].append(v)
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
@@ -105,6 +109,10 @@ def main():
             cyc = m["GRBM_GUI_ACTIVE"] / XCDS
             e["mfma_util"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS_PER_XCD * XCDS)
             e["gpu_cycles"] = cyc
+            if m.get("dispatch_ns"):
+                # effective shader clock of the profiled dispatch (MI355X_MICROARCH "DVFS give-back":
+                # GRBM_GUI_ACTIVE / 8 / wall time; profiled passes run a few % below un-profiled ones)
+                e["clock_GHz"] = cyc / m["dispatch_ns"]
         if k in mops:
             # MFMA work the kernel executed (512 ops per MOPS unit), against what bench credits it
             m = mops[k]
