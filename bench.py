@@ -535,6 +535,10 @@ def main():
             if tr.get("source_sha256") == source_hash() and tr.get("shape") == [B, H, S, D]:
                 out["roofline"]["traffic"] = tr["traffic"].get(dom)
                 out["roofline"]["traffic_source"] = tr.get("tag")
+                # effective shader clock of the kernel's profiled dispatch (GRBM_GUI_ACTIVE / 8 /
+                # dispatch time); the peak above assumes 2.4 GHz
+                if tr.get("clock_GHz", {}).get(dom):
+                    out["roofline"]["clock_GHz_profiled"] = tr["clock_GHz"][dom]
             else:
                 out["roofline"]["traffic_note"] = "PMC traffic in profiles/ is from other sources: omitted"
         except Exception:

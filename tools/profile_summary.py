@@ -132,7 +132,9 @@ def main():
     with open(os.path.join(out_dir, "traffic_latest.json"), "w") as f:
         # bench.py reports these only while the kernel sources hash to source_sha256
         json.dump({"tag": tag, "source_sha256": source_hash(), "shape": [4, 32, 4096, 128],
-                   "traffic": traffic}, f, indent=1)
+                   "traffic": traffic,
+                   "clock_GHz": {k: e["clock_GHz"] for k, e in out.items() if "clock_GHz" in e}},
+                  f, indent=1)
     print(json.dumps(out, indent=1))
 
 
