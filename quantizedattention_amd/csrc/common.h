@@ -449,10 +449,15 @@ QA_DEVICE void glds4_s(const void* sbase, unsigned voff, void* lds_base) {
 // LDS-ring step: wait until at most N of this wave's VMEM ops (the LDS-DMA of later tiles) are in
 // flight and all its LDS reads returned, then workgroup barrier (publishes the landed tile and
 // frees the oldest slot).
+// (-DQA_RING_DRAIN=1, diagnostic builds: wait for every VMEM op instead -- no DMA in flight across a
+// barrier, which rules the ring's wait counts out as the cause of a result)
+#ifndef QA_RING_DRAIN
+#define QA_RING_DRAIN 0
+#endif
 template <int N>
 QA_DEVICE void ring_wait_barrier() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(QA_RING_DRAIN ? 0 : N) : "memory");
 }
 // ---------------------------------------------------------------- buffer LDS-DMA (ring staging)
 // buffer_load_dword{x4} ... offen lds: source = V#.base + voffset (lane-constant, swizzle applied)

@@ -621,11 +621,17 @@ void int8_bwd_kernel(
       }
 #endif
       // record of (query head bh*G + t/nqt, q-tile t%nqt, key tile x0/32), relative to this key/value
-      // head's first record (ws_rsrc / sc_rsrc): SGPR offsets, no per-lane address arithmetic
+      // head's first record (ws_rsrc / sc_rsrc)
       const int nqt = Smod / 32, nkt = Sx / 32;
       const unsigned rel = (unsigned)(t * nkt + x0 / 32);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, bytes), ws_rsrc, 16 * lane,
-                                             (int)(rel * 1024u), 0);
+      // The tile offset goes in the VGPR offset with soffset = 0: hipcc pads a VALU write of the
+      // data registers of a > 64-bit buffer store only when soffset is not a register, while on
+      // gfx950 the hazard holds either way.  With the offset in an SGPR the next instruction (a
+      // v_and into the register of dword 0) overwrote the data before the store read it: dword 0
+      // of some records of the last query tile came out wrong, run-dependently, at D = 64
+      // (tools/nondet_probe3.py; tests/test_gpu_int8_ext.py::test_int8_bwd_ws_long_d64).
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, bytes), ws_rsrc,
+                                             16 * lane + (int)(rel * 1024u), 0, 0);
       (void)nqt;
       if (lane == 0) sds_lds[wave * nt + t] = sx;   // written out after the loop
     }

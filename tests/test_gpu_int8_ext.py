@@ -148,6 +148,29 @@ def test_int8_bwd_ws_bit_identical_large(lib):
         assert torch.equal(x, y), name
 
 
+@pytest.mark.parametrize("shape,causal", [((2, 6, 6, 3840, 3840, 64), False), ((2, 8, 2, 1024, 1024, 64), True),
+                                          ((2, 6, 6, 4096, 4096, 64), True)])
+def test_int8_bwd_ws_long_d64(lib, shape, causal):
+    """Long sequences at D = 64, where the dS record store of the last query tile was once followed
+    directly by a VALU write of its data register (a store-data hazard hipcc did not pad for an
+    SGPR soffset): dword 0 of some records came out wrong, run-dependently, and dq of that tile's
+    first 8 rows with it.  Four record runs against the recomputing backward, bit for bit."""
+    from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward
+    B, Hq, Hkv, Sq, Sk, D = shape
+    g = torch.Generator(device="cuda").manual_seed(0)
+    q = torch.randn((B, Hq, Sq, D), device="cuda", generator=g).half()
+    k, v = (torch.randn((B, Hkv, Sk, D), device="cuda", generator=g).half() for _ in range(2))
+    dO = torch.randn((B, Hq, Sq, D), device="cuda", generator=g).half()
+    O, lse, qi, kiT, vi, sq, sk, sv, _, qb, kb = _int8_forward(q, k, v, smooth=True, images=True, causal=causal)
+    kw = dict(causal=causal, kv_heads=Hkv, ws_chunk=0)
+    ref = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb, kb, use_ws=False, **kw)
+    for poison in (None, 0x00, 0x7F, 0x81):
+        out = _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb, kb, use_ws=True, ws_poison=poison, **kw)
+        torch.cuda.synchronize()
+        for name, a, b in zip(("dq", "dk", "dv"), out, ref):
+            assert torch.equal(a, b), (name, poison, int((a != b).sum()))
+
+
 @pytest.mark.parametrize("shape,causal", [((2, 6, 3, 256, 256, 64), True), ((1, 8, 2, 512, 512, 128), True),
                                           ((2, 4, 4, 256, 256, 128), False)])
 def test_int8_bwd_run_to_run_identical(lib, shape, causal):

@@ -102,3 +102,38 @@ def test_checker_flags_a_compiler_m0_use():
     assert bad and "compiler-emitted" in bad[0]
     n, bad = _check(";;#ASMSTART\n\tbuffer_load_dword v1, s[0:3], s5 offen lds\n;;#ASMEND\n")
     assert bad and "without an M0 write" in bad[0]
+
+
+# A buffer store of more than 64 bits of data, and the instructions after it.  hipcc pads a VALU write
+# of the store's data registers only when soffset is not a register; on gfx950 the hazard holds with
+# an SGPR soffset too (a record store followed directly by a v_and into its dword-0 register stored
+# the new value, run-dependently: tests/test_gpu_int8_ext.py::test_int8_bwd_ws_long_d64).  So every
+# such store must use an inline-constant soffset, which the compiler then protects.
+WIDE_STORE = re.compile(r"^\s*buffer_store_(dwordx[34]|b96|b128)\s+v\[\d+:\d+\],\s*\S+,\s*s\[\d+:\d+\],\s*(\S+)")
+
+
+def _wide_store_violations(text: str) -> tuple[int, list[str]]:
+    bad, n = [], 0
+    for no, line in enumerate(text.split("\n"), 1):
+        m = WIDE_STORE.match(line.split(";")[0])
+        if m:
+            n += 1
+            soff = m.group(2).rstrip(",")
+            if re.fullmatch(r"s\d+|s\[\d+:\d+\]|m0|vcc\w*|ttmp\d+", soff):
+                bad.append(f"line {no}: wide buffer store with a register soffset: {line.strip()!r}")
+    return n, bad
+
+
+def test_wide_buffer_stores_use_a_constant_soffset(asm):
+    total = 0
+    for name, text in asm.items():
+        n, bad = _wide_store_violations(text)
+        total += n
+        assert not bad, f"{name}: " + "; ".join(bad[:3])
+    assert total > 0, "no wide buffer store found: the pattern no longer matches the emitted code"
+
+
+def test_checker_flags_a_register_soffset():
+    assert _wide_store_violations("\tbuffer_store_dwordx4 v[112:115], v117, s[4:7], 0 offen\n") == (1, [])
+    n, bad = _wide_store_violations("\tbuffer_store_dwordx4 v[112:115], v137, s[24:27], s58 offen\n")
+    assert n == 1 and bad
