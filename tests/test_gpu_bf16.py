@@ -118,7 +118,7 @@ def test_bf16_gqa_fwd_bwd(lib, hq, hkv, sq, sk, causal):
 @pytest.mark.parametrize("hq,hkv,sq,sk,d,causal", [
     (2, 2, 256, 256, 128, False), (2, 2, 256, 256, 128, True), (4, 2, 160, 224, 128, False),
     (4, 1, 96, 192, 128, True), (2, 2, 192, 320, 64, False), (3, 3, 128, 128, 64, True),
-    (2, 1, 1024, 1024, 128, True)])
+    (2, 1, 1024, 1024, 128, True), (4, 4, 4096, 4096, 64, False), (6, 2, 3840, 3840, 64, True)])
 def test_bf16_bwd_fused_dkdv_bit_identical(lib, monkeypatch, hq, hkv, sq, sk, d, causal):
     """The fused dK+dV path (default: dQ recomputes dS), its dS-record variant (dQ reads bf16 dS
     records) and the split dV / dK kernels give identical gradients (same P / dS operands and
