@@ -1,6 +1,6 @@
 """Causal int8 record backward: time + output hash per head-chunk size, for A/B of dK+dV grid
-variants (the paired grid of DESIGN.md §5 round 3 was measured with it; that variant is in git
-history).  Run through tools/ab_run.sh; equal hashes across variants = bit-identical gradients.
+variants (the paired grid of DESIGN.md §5 round 3 was measured with it and not kept; DESIGN.md
+describes how it was built).  Run through tools/ab_run.sh; equal hashes across variants = bit-identical gradients.
 
     python tools/ab_pair.py            (env CHUNKS="0,32,64": key/value heads per chunk, 0 = one pass)"""
 import hashlib, os, sys, torch
