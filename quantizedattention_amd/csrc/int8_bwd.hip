@@ -625,11 +625,12 @@ void int8_bwd_kernel(
       const int nqt = Smod / 32, nkt = Sx / 32;
       const unsigned rel = (unsigned)(t * nkt + x0 / 32);
       // The tile offset goes in the VGPR offset with soffset = 0: hipcc pads a VALU write of the
-      // data registers of a > 64-bit buffer store only when soffset is not a register, while on
-      // gfx950 the hazard holds either way.  With the offset in an SGPR the next instruction (a
-      // v_and into the register of dword 0) overwrote the data before the store read it: dword 0
-      // of some records of the last query tile came out wrong, run-dependently, at D = 64
-      // (tools/nondet_probe3.py; tests/test_gpu_int8_ext.py::test_int8_bwd_ws_long_d64).
+      // data registers of a > 64-bit buffer store (2 wait states) only when soffset is not a
+      // register, while on gfx950 the hazard holds either way.  With the offset in an SGPR the
+      // second instruction after the store (a v_and into the register of dword 0) overwrote the data
+      // before the store read it: dword 0 of some records of the last query tile came out wrong,
+      // run-dependently, at D = 64 (tools/nondet_probe3.py; tests/test_gpu_int8_ext.py::
+      // test_int8_bwd_ws_long_d64; tests/test_isa.py checks the emitted code).
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, bytes), ws_rsrc,
                                              16 * lane + (int)(rel * 1024u), 0, 0);
       (void)nqt;

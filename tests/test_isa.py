@@ -138,3 +138,59 @@ def test_checker_flags_a_register_soffset():
     n, bad = _wide_store_violations("\tbuffer_store_dwordx4 v[112:115], v137, s[24:27], s58 offen\n")
     assert n == 1 and bad
 
+
+
+# The symptom itself, however the store is addressed: the data registers of a > 64-bit store written
+# by a VALU within two wait states of the store (s_nop N counts N + 1).  hipcc keeps every padded wide
+# store at distance >= 3 (global stores: an s_nop 1 where needed); the pre-fix record store had its
+# dword-0 register rewritten by the second instruction after it.  Linear order is checked, which is
+# execution order on the fall-through path.
+_WIDE_ANY = re.compile(r"^(global_store_dwordx[34]|flat_store_dwordx[34]|buffer_store_dwordx[34]|"
+                       r"global_store_b(96|128)|buffer_store_b(96|128))\s")
+
+
+def _vregs(spec: str) -> set[int]:
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", spec)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.fullmatch(r"v(\d+)", spec)
+    return {int(m.group(1))} if m else set()
+
+
+def _store_data_overwrites(text: str) -> tuple[int, list[str]]:
+    code = [ln.split(";")[0].strip() for ln in text.split("\n")]
+    code = [c for c in code if c and not c.startswith(".") and not c.endswith(":")]
+    n, bad = 0, []
+    for i, c in enumerate(code):
+        if not _WIDE_ANY.match(c):
+            continue
+        n += 1
+        ops = [t.strip(",") for t in c.split()[1:]]
+        data = _vregs(ops[1] if c.startswith(("global", "flat")) else ops[0])
+        dist = 0
+        for nxt in code[i + 1:i + 4]:
+            dist += int(nxt.split()[1]) + 1 if nxt.startswith("s_nop") else 1
+            if dist > 2:
+                break
+            if (nxt.startswith("v_") and not nxt.startswith(("v_readlane", "v_readfirstlane"))
+                    and _vregs(nxt.split()[1].strip(",")) & data):
+                bad.append(f"{c!r} then {nxt!r} at distance {dist}")
+                break
+    return n, bad
+
+
+def test_no_wide_store_data_overwritten_within_two_wait_states(asm):
+    total = 0
+    for name, text in asm.items():
+        n, bad = _store_data_overwrites(text)
+        total += n
+        assert not bad, f"{name}: " + "; ".join(bad[:3])
+    assert total > 0
+
+
+def test_checker_flags_a_close_overwrite():
+    old = ("\tbuffer_store_dwordx4 v[114:117], v143, s[24:27], s2 offen\n"
+           "\tv_and_b32_e32 v97, 0x7fffffff, v70\n\tv_and_b32_e32 v114, 0x7fffffff, v71\n")
+    new = ("\tbuffer_store_dwordx4 v[112:115], v117, s[4:7], 0 offen\n\ts_nop 1\n"
+           "\tv_and_b32_e32 v112, 0x7fffffff, v68\n")
+    assert _store_data_overwrites(old)[1] and not _store_data_overwrites(new)[1]
