@@ -64,6 +64,11 @@ QA_DEVICE void quant_operand(const float* x, float inv, float c, v8bf* out) {
 }
 
 // ------------------------------------------------------------------------------------ prep
+// QA_PREP_HOIST: all loads of a block before its arithmetic (bit-identical; bwd_prep 100 -> 93-95 us
+// at config 3, tools/ab_quant.py); 0 = the per-row-group order hipcc serialises on the LD stores
+#ifndef QA_PREP_HOIST
+#define QA_PREP_HOIST 1
+#endif
 // One wave per 32-row block of dO (and O), one pass over both:
 //   sdO = f16(amax|dO| / 127), dO_i8 = trunc(f16(dO / sdO))      (int8:372-374, same quantiser)
 //   img = bf16(dO_i8)  (exact; the dV product's transposed-read image; optional)
@@ -83,11 +88,29 @@ __global__ __launch_bounds__(256) void int8_bwd_prep_kernel(
   const _Float16* ob = O + blk * ELEMS;
   v8h v[ITERS];
   float amax = 0.f;
+#if QA_PREP_HOIST
+  // every load of the block first (dO, O and the lse of the lane's row group), then the arithmetic:
+  // one HBM round trip per wave instead of one per row group (hipcc otherwise keeps each group's
+  // loads behind the previous group's LD store)
+  v8h ov[ITERS];
+  _Float16 lsev[ITERS];
 #pragma unroll
   for (int i = 0; i < ITERS; ++i) {
     const int e = (i * 64 + lane) * 8;
     v[i] = *reinterpret_cast<const v8h*>(xb + e);
+    ov[i] = *reinterpret_cast<const v8h*>(ob + e);
+    lsev[i] = lse[blk * 32 + e / D];
+  }
+#endif
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int e = (i * 64 + lane) * 8;
+#if QA_PREP_HOIST
+    const v8h o = ov[i];
+#else
+    v[i] = *reinterpret_cast<const v8h*>(xb + e);
     const v8h o = *reinterpret_cast<const v8h*>(ob + e);
+#endif
     float dsum = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -98,7 +121,11 @@ __global__ __launch_bounds__(256) void int8_bwd_prep_kernel(
     for (int m = TPR / 2; m >= 1; m >>= 1) dsum += __shfl_xor(dsum, m);
     if (lane % TPR == 0) {
       const long row = blk * 32 + e / D;
+#if QA_PREP_HOIST
+      LD[row] = float2{(float)lsev[i], (float)(_Float16)dsum};
+#else
       LD[row] = float2{(float)lse[row], (float)(_Float16)dsum};
+#endif
     }
   }
   amax = wave_max_f(amax);
