@@ -66,6 +66,11 @@ int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt, long rows
  * order).  rows % 32 == 0. */
 int qattn_int8_quant_vop(const void* v, void* v_i8, void* sv, void* vop, long rows, int head_dim,
                          void* stream);
+/* The same as qattn_int8_quant_vop with the keys of each 16-key k-step in the forward's accumulator
+ * order: piece 4 s2 + b lane L = 32h + i holds vdq[row 16 s2 + 8(j >> 2) + 4h + (j & 3)][32b + i],
+ * j = 0..7 -- the V^T operand of qattn_int8_attn_fwd_vpo_ex. */
+int qattn_int8_quant_vpo(const void* v, void* v_i8, void* sv, void* vpo, long rows, int head_dim,
+                         void* stream);
 /* vt of qattn_int8_quant_vt from stored indices v_i8 (a restored int8 key/value cache). */
 int qattn_int8_v_image(const void* v_i8, void* vt, long rows, int head_dim, void* stream);
 
@@ -101,6 +106,14 @@ int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, const void* k_
                                 const void* vt, const void* sv, void* out, void* lse, long bh,
                                 long sq_tok, long sk_tok, int group, int causal, int head_dim,
                                 float qks, void* stream);
+
+/* qattn_int8_attn_fwd_ex (f16 P.V: one f16 MFMA on f16(P_i8 * sp) x f16(v_i8 * sv)) with the V
+ * operand read from vpo, the operand-order image of qattn_int8_quant_vpo.  Same outputs and
+ * conventions as qattn_int8_attn_fwd_ex. */
+int qattn_int8_attn_fwd_vpo_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
+                               const void* vpo, void* out, void* lse, long bh, long sq_tok,
+                               long sk_tok, int group, int causal, int head_dim, float qks,
+                               void* stream);
 
 /* Role-split form of the int8 forward (attention_int8.py:197-257; csrc/int8_attn_fwd_rs.hip): per
  * SIMD one wave issues the MFMAs (QK^T on the int8 MFMA, P.V on f16(P_i8 sp) x f16(v_i8 sv)) and two
@@ -173,8 +186,8 @@ int qattn_int8_attn_bwd_ex(const void* dO_i8, const void* sdO, const void* q_i8,
  * (overwritten, not read before written).  Returns 1 for ws == NULL. */
 long qattn_int8_bwd_ws_bytes(long bh, long sq_tok, long sk_tok);
 /* The largest dS-record workspace the backwards (int8 and bf16 alike) allocate before they fall back
- * to recomputation: QATTN_BWD_WS_MAX bytes if that is set, else min(16 GiB, half the free device
- * memory at the call). */
+ * to recomputation: QATTN_BWD_WS_MAX bytes if that is set, else 16 GiB (a workspace allocation
+ * that fails also falls back to recomputation). */
 long qattn_bwd_ws_cap(void);
 int qattn_int8_attn_bwd_ws(const void* dO_i8, const void* sdO, const void* q_i8, const void* sq,
                            const void* k_i8, const void* sk, const void* v_i8, const void* sv,

@@ -27,10 +27,12 @@ SIGNATURES = {
     "qattn_int8_dequant": [_vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_int8_quant_vt": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_int8_quant_vop": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
+    "qattn_int8_quant_vpo": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_int8_v_image": [_vp, _vp, _c_long, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_int8_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
+    "qattn_int8_attn_fwd_vpo_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_i8pv_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                  _vp],
     "qattn_int8_attn_fwd_rs": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],

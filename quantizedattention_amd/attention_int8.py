@@ -151,8 +151,8 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
 # Largest dS workspace (bytes) the backward allocates to skip the dQ pass's recomputation of S,
 # dP, P and dS (qattn_int8_attn_bwd_ws); larger problems recompute (qattn_int8_attn_bwd_ex).  The
 # results are bit-identical either way.  1 B per score + 4 B per 32x32 tile: 2.2 GB at (4,32,4096).
-# None: the library's shared cap (qattn_bwd_ws_cap: QATTN_BWD_WS_MAX, else min(16 GiB, half the free
-# device memory)), the same rule as the bf16 backward and the C++ operators.
+# None: the library's shared cap (qattn_bwd_ws_cap: QATTN_BWD_WS_MAX, else 16 GiB; an allocation that
+# fails falls back to recomputation), the same rule as the bf16 backward and the C++ operators.
 WS_MAX_BYTES = None
 # Key/value heads per chunk of the record backward (qattn_int8_attn_bwd_wsc): dK+dV then dQ per
 # chunk, one chunk-sized workspace re-used by every chunk; 0: one pass over all heads; unset: auto

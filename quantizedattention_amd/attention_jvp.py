@@ -125,10 +125,15 @@ def _key(q, k, v):
 
 def _jvp_follows(tensors) -> bool:
     """True when the Function's jvp rule will run right after its forward: the innermost functorch
-    transform is torch.func.jvp, or (no functorch transform) an input is a forward-AD dual tensor."""
+    transform is torch.func.jvp AND an input is wrapped at that transform's level (so it carries a
+    tangent there), or (no functorch transform) an input is a forward-AD dual tensor."""
     if torch._C._functorch.peek_interpreter_stack() is not None:
         from torch._functorch.pyfunctorch import retrieve_current_functorch_interpreter
-        return retrieve_current_functorch_interpreter().key() == torch._C._functorch.TransformType.Jvp
+        interp = retrieve_current_functorch_interpreter()
+        if interp.key() != torch._C._functorch.TransformType.Jvp:
+            return False
+        level = interp.level()
+        return any(torch._C._functorch.maybe_get_level(t) == level for t in tensors)
     import torch.autograd.forward_ad as fwAD
     return any(fwAD.unpack_dual(t).tangent is not None for t in tensors)
 
@@ -151,7 +156,7 @@ class AttentionJVP_autograd_function(torch.autograd.Function):
             with torch._C._DisableFuncTorch():
                 B, H, S, D = q.shape
                 O = torch.empty((B, H, S, D), dtype=torch.float32, device=q.device)
-            _DEFER.pending = getattr(_DEFER, "pending", []) + [(_key(q, k, v), O)]
+            _DEFER.pending = getattr(_DEFER, "pending", []) + [(_key(q, k, v), O, (q, k, v))]
             return O
         with torch._C._DisableFuncTorch():
             O, _tO, _lse = _jvp(q, k, v, None)
@@ -176,7 +181,7 @@ class AttentionJVP_autograd_function(torch.autograd.Function):
         # a deferred forward's O (see forward): filled here by the same launch as tO
         out_O = None
         pending = getattr(_DEFER, "pending", [])
-        for i, (key, O) in enumerate(pending):
+        for i, (key, O, _) in enumerate(pending):
             if key == _key(q, k, v):
                 out_O = O
                 _DEFER.pending = pending[:i] + pending[i + 1:]
@@ -194,8 +199,19 @@ def attention_jvp(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> torch.Te
     """O fp32 [B,H,S,D]; differentiable in forward mode through the HIP tangent kernel (one launch
     per torch.func.jvp / forward-AD call)."""
     prev = getattr(_DEFER, "on", False)
-    _DEFER.on = _jvp_follows((q, k, v))
+    defer = _jvp_follows((q, k, v))
+    _DEFER.on = defer
+    n0 = len(getattr(_DEFER, "pending", []))
     try:
-        return AttentionJVP_autograd_function.apply(q, k, v)
+        out = AttentionJVP_autograd_function.apply(q, k, v)
     finally:
         _DEFER.on = prev
+        # no deferred entry outlives the call that made it
+        pending = getattr(_DEFER, "pending", [])
+        left, _DEFER.pending = pending[n0:], pending[:n0]
+    # a deferred O whose jvp rule did not run (no tangent reached this call after all) is filled by
+    # the primal kernel
+    for _k, O, (pq, pk, pv) in left:
+        with torch._C._DisableFuncTorch():
+            _jvp(pq, pk, pv, None, out_O=O)
+    return out

@@ -78,7 +78,10 @@ def build_c_host(verbose: bool = True) -> Path | None:
            "-Wl,-rpath,$ORIGIN/../../quantizedattention_amd"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"C host build failed:\n{r.stderr}")
+        # a test program, not part of the library: its link failing must not fail the build
+        # (tests/test_gpu_c_abi.py, which needs it, reports the missing program)
+        print(f"[qattn build] warning: C host program not built:\n{r.stderr}", file=sys.stderr)
+        return None
     os.replace(str(C_HOST_BIN) + ".tmp", C_HOST_BIN)
     if verbose:
         print(f"[qattn build] linked {C_HOST_BIN}", file=sys.stderr)

@@ -1205,14 +1205,14 @@ static bool ws_region_fits(long group, long sq_tok, long sk_tok) {
 }
 
 // Largest dS-record workspace either backward (int8 or bf16) allocates before it falls back to
-// recomputation: QATTN_BWD_WS_MAX bytes if set, else min(16 GiB, half the device memory free now).
+// recomputation: QATTN_BWD_WS_MAX bytes if set, else 16 GiB.  A fixed figure, not the device's free
+// memory: hipMemGetInfo does not see what the caller's caching allocator holds reserved, so a free-
+// memory cap would depend on allocator history; an allocation that fails falls back to the
+// recomputing backward instead (same results).
 extern "C" long qattn_bwd_ws_cap(void) {
   const char* s = getenv("QATTN_BWD_WS_MAX");
   if (s != nullptr && *s != 0) return strtol(s, nullptr, 10);
-  long cap = 16L << 30;
-  size_t free_b = 0, total_b = 0;
-  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && (long)(free_b / 2) < cap) cap = (long)(free_b / 2);
-  return cap;
+  return 16L << 30;
 }
 
 extern "C" long qattn_int8_bwd_ws_bytes(long bh, long sq_tok, long sk_tok) {

@@ -125,7 +125,10 @@ __global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restric
 // halves vdq[key 16 s2 + 8h + j][32b + i], j = 0..7 -- the A operand of v_mfma_f32_32x32x16_f16
 // for V^T, keys in natural order.  The block's vdq goes through a swizzled row-major LDS image and
 // comes back transposed by ds_read_b64_tr_b16 (two reads of 4 keys per operand).
-template <int D>
+// PERM: the keys of each 16-key k-step in the order of the S^T accumulator of the mixed-wave forward
+// (common.h: slot j of half h holds key 8(j >> 2) + 4h + (j & 3)), so that the accumulator's f16 P
+// operand needs no reordering (qattn_int8_quant_vpo, the f16 P.V mode of int8_attn_fwd.hip).
+template <int D, bool PERM = false>
 __global__ __launch_bounds__(256) void quant_vop_kernel(const _Float16* __restrict__ v,
                                                         int8_t* __restrict__ vi,
                                                         _Float16* __restrict__ sv,
@@ -176,10 +179,10 @@ __global__ __launch_bounds__(256) void quant_vop_kernel(const _Float16* __restri
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
     for (int b = 0; b < NDB; ++b) {
-      const int key = 16 * s2 + 8 * h + (i16 >> 2);
+      const int key = 16 * s2 + (PERM ? 4 : 8) * h + (i16 >> 2);
       const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
       const char* a = im + key * 2 * D + 16 * ((d / 8) ^ sw(key)) + (d % 8) * 2;
-      const v8s t = ds_read_tr16_x2(a, a + 4 * 2 * D);
+      const v8s t = ds_read_tr16_x2(a, a + (PERM ? 8 : 4) * 2 * D);
       *reinterpret_cast<v8s*>(reinterpret_cast<char*>(vop) + blk * ELEMS * 2 + (s2 * NDB + b) * 1024 +
                               16 * lane) = t;
     }
@@ -315,6 +318,22 @@ extern "C" int qattn_int8_quant_vop(const void* v, void* v_i8, void* sv, void* v
   else
     hipLaunchKernelGGL(quant_vop_kernel<64>, grid, block, 0, st, (const _Float16*)v, (int8_t*)v_i8,
                        (_Float16*)sv, (_Float16*)vop, nblocks);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_int8_quant_vpo(const void* v, void* v_i8, void* sv, void* vpo, long rows,
+                                    int head_dim, void* stream) {
+  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  const long nblocks = rows / 32;
+  if (nblocks == 0) return 0;
+  dim3 grid((unsigned)((nblocks + 3) / 4)), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (head_dim == 128)
+    hipLaunchKernelGGL((quant_vop_kernel<128, true>), grid, block, 0, st, (const _Float16*)v,
+                       (int8_t*)v_i8, (_Float16*)sv, (_Float16*)vpo, nblocks);
+  else
+    hipLaunchKernelGGL((quant_vop_kernel<64, true>), grid, block, 0, st, (const _Float16*)v,
+                       (int8_t*)v_i8, (_Float16*)sv, (_Float16*)vpo, nblocks);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

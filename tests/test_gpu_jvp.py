@@ -101,6 +101,25 @@ def test_jvp_autograd_function_forward_mode(lib, dtype):
     assert (tO.cpu() - tOt).abs().max().item() <= tol * max(1.0, tOt.abs().max().item())
 
 
+def test_jvp_constant_inputs_under_transform(lib):
+    """attention_jvp on inputs that carry no tangent at the current torch.func.jvp level
+    (the primal of the transformed function is something else) must return the real O, not the
+    deferred forward's empty buffer, and leave no pending entry behind."""
+    from quantizedattention_amd import attention_jvp as J
+    from quantizedattention_amd.attention_jvp import attention_jvp, helion_attention_jvp_forward_fp32
+    g = torch.Generator().manual_seed(9)
+    shape = (1, 2, 64, 64)
+    q0, k0, v0 = (torch.randn(shape, generator=g).cuda() for _ in range(3))
+    x, tx = (torch.randn(shape, generator=g).cuda() for _ in range(2))
+    O_ref, _, _ = helion_attention_jvp_forward_fp32(q0, k0, v0, *(torch.zeros_like(q0),) * 3)
+    for _ in range(3):   # repeated calls: a stale entry would be matched by reused addresses
+        y, ty = torch.func.jvp(lambda a: attention_jvp(q0, k0, v0) + a, (x,), (tx,))
+        torch.cuda.synchronize()
+        assert torch.equal(y, O_ref + x)
+        assert torch.equal(ty, tx)
+        assert not getattr(J._DEFER, "pending", [])
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape", [(1, 4, 2, 128, 128, 128), (2, 6, 3, 64, 192, 64)])
 def test_jvp_grouped_query(lib, dtype, shape):

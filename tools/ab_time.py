@@ -53,6 +53,10 @@ call("qattn_int8_quant", P(k), P(ki), P(sk), None, None, N, S, D, st)
 call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 if entry("qattn_int8_quant_vt") is not None:
     call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
+vpo = None
+if entry("qattn_int8_quant_vpo") is not None:
+    vpo = e(N, D, dt=torch.float16)
+    call("qattn_int8_quant_vpo", P(v), P(vi), P(sv), P(vpo), N, D, st)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
 fns = {}
 if entry("qattn_int8_attn_fwd_ex") is not None:
@@ -61,6 +65,9 @@ if entry("qattn_int8_attn_fwd_ex") is not None:
 if entry("qattn_int8_attn_fwd_i8pv_ex") is not None:
     fns["i8"] = lambda: call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv),
                              P(O), P(lse), B * H, S, S, 1, int(causal), D, qks, st)
+if entry("qattn_int8_attn_fwd_vpo_ex") is not None:
+    fns["vpo"] = lambda: call("qattn_int8_attn_fwd_vpo_ex", P(qi), P(sq), P(ki), P(sk), P(vpo), P(O), P(lse),
+                              B * H, S, S, 1, int(causal), D, qks, st)
 if entry("qattn_int8_attn_fwd_f2") is not None and not causal:
     fns["f2"] = lambda: call("qattn_int8_attn_fwd_f2", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse),
                              B * H, S, S, 1, D, qks, st)
@@ -88,5 +95,11 @@ for mode, f in fns.items():
     import hashlib
     digest = hashlib.sha256(O.view(torch.int16).cpu().numpy().tobytes() +
                             lse.view(torch.int16).cpu().numpy().tobytes()).hexdigest()[:12]
+    ref_o = globals().setdefault("_ref_o", {})
+    if not ref_o:
+        ref_o["o"], ref_o["l"], ref_o["m"] = O.float().clone(), lse.float().clone(), mode
+    dO = (O.float() - ref_o["o"]).abs().max().item()
+    dl = (lse.float() - ref_o["l"]).abs().max().item()
+    print(f"  max|O - O[{ref_o['m']}]| = {dO:.3g}, max|lse - lse[{ref_o['m']}]| = {dl:.3g}")
     print(f"{name} pv={mode}{' causal' if causal else ''}: {t * 1e3:.1f} us  {ops / t / 1e9:.0f} TOPS "
           f"({ops / t / 1e9 / 5033 * 100:.1f}% i8 peak)  O/lse {digest}", flush=True)
