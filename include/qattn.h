@@ -59,18 +59,6 @@ int qattn_int8_dequant(const void* idx, const void* scale, void* deq, long rows,
  *   v_mfma_i32_32x32x32_i8 in the forward's key order).  rows % 32 == 0. */
 int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt, long rows, int head_dim,
                         void* stream);
-/* V quantiser (same indices and scales as qattn_int8_quant) that also writes the f16 P.V operand
- * image of the role-split forward (qattn_int8_attn_fwd_rs): vop f16 [rows/32][2 D/32][64][8], for
- * each 32-row block, piece 4 s2 + b (b < D/32) lane L = 32h + i holds vdq[row 16 s2 + 8h + j][32b + i],
- * j = 0..7, vdq = f16(v_i8 * sv) (the A operand of v_mfma_f32_32x32x16_f16 for V^T, natural key
- * order).  rows % 32 == 0. */
-int qattn_int8_quant_vop(const void* v, void* v_i8, void* sv, void* vop, long rows, int head_dim,
-                         void* stream);
-/* The same as qattn_int8_quant_vop with the keys of each 16-key k-step in the forward's accumulator
- * order: piece 4 s2 + b lane L = 32h + i holds vdq[row 16 s2 + 8(j >> 2) + 4h + (j & 3)][32b + i],
- * j = 0..7 -- the V^T operand of qattn_int8_attn_fwd_vpo_ex. */
-int qattn_int8_quant_vpo(const void* v, void* v_i8, void* sv, void* vpo, long rows, int head_dim,
-                         void* stream);
 /* vt of qattn_int8_quant_vt from stored indices v_i8 (a restored int8 key/value cache). */
 int qattn_int8_v_image(const void* v_i8, void* vt, long rows, int head_dim, void* stream);
 
@@ -106,32 +94,6 @@ int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, const void* k_
                                 const void* vt, const void* sv, void* out, void* lse, long bh,
                                 long sq_tok, long sk_tok, int group, int causal, int head_dim,
                                 float qks, void* stream);
-
-/* qattn_int8_attn_fwd_ex (f16 P.V: one f16 MFMA on f16(P_i8 * sp) x f16(v_i8 * sv)) with the V
- * operand read from vpo, the operand-order image of qattn_int8_quant_vpo.  Same outputs and
- * conventions as qattn_int8_attn_fwd_ex. */
-int qattn_int8_attn_fwd_vpo_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                               const void* vpo, void* out, void* lse, long bh, long sq_tok,
-                               long sk_tok, int group, int causal, int head_dim, float qks,
-                               void* stream);
-
-/* Role-split form of the int8 forward (attention_int8.py:197-257; csrc/int8_attn_fwd_rs.hip): per
- * SIMD one wave issues the MFMAs (QK^T on the int8 MFMA, P.V on f16(P_i8 sp) x f16(v_i8 sv)) and two
- * waves the softmax (f16 S rounding, row max, deferred running max, exp2, P_i8), handing tiles over
- * through LDS.  vop = the operand image of qattn_int8_quant_vop.  Non-causal; head_dim 128; the
- * numerics of qattn_int8_attn_fwd_ex (f16 P.V mode).  Same outputs and other conventions as
- * qattn_int8_attn_fwd_ex.  Returns 1 for other shapes (callers use qattn_int8_attn_fwd_i8pv_ex). */
-int qattn_int8_attn_fwd_rs(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                           const void* vop, void* out, void* lse, long bh, long sq_tok, long sk_tok,
-                           int group, int head_dim, float qks, void* stream);
-
-/* qattn_int8_attn_fwd_ex (f16 P.V: vdq = the f16 image of qattn_int8_quant) on a schedule
- * software-pipelined by two key tiles (csrc/int8_attn_fwd_f2.hip): the softmax of tile t runs beside
- * the MFMAs of QK^T(t+1) and P.V(t-1).  Non-causal; head_dim 64 / 128; bit-identical to the f16 P.V
- * mode with the biased S accumulator.  Returns 1 for causal-only or unsupported shapes. */
-int qattn_int8_attn_fwd_f2(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                           const void* vdq, void* out, void* lse, long bh, long sq_tok, long sk_tok,
-                           int group, int head_dim, float qks, void* stream);
 
 /* Key-split (flash-decoding) form of qattn_int8_attn_fwd_i8pv_ex, non-causal, for short query blocks
  * against long key ranges (the int8 key/value cache): each workgroup covers

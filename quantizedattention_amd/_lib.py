@@ -26,17 +26,12 @@ SIGNATURES = {
     "qattn_int8_quant_img": [_vp] * 6 + [_c_long, _c_int, _c_int, _vp],
     "qattn_int8_dequant": [_vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_int8_quant_vt": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
-    "qattn_int8_quant_vop": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
-    "qattn_int8_quant_vpo": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_int8_v_image": [_vp, _vp, _c_long, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_int8_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
-    "qattn_int8_attn_fwd_vpo_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_i8pv_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                  _vp],
-    "qattn_int8_attn_fwd_rs": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
-    "qattn_int8_attn_fwd_f2": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_split": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                _vp],
     "qattn_int8_split_combine": [_vp] * 4 + [_c_long, _c_int, _c_int, _vp],

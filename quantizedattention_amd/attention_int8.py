@@ -59,16 +59,13 @@ def _check_shapes(q, k, v):
         raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
 
 
-# P.V contraction of the forward (csrc/int8_attn_fwd.hip, csrc/int8_attn_fwd_rs.hip):
+# P.V contraction of the forward (csrc/int8_attn_fwd.hip):
 #   "i8": v_mfma_i32_32x32x32_i8 on P_i8 x v_i8, as the reference's hl.dot (int8:249), with one fused
 #         dequantisation per 32-key tile;
-#   "f16": v_mfma_f32_32x32x16_f16 on f16(P_i8 * sp) x f16(v_i8 * sv), the tile scale in the operands;
-#   "rs": the f16 contraction in the role-split kernel (one MFMA wave and two softmax waves per SIMD)
-#         where it applies (non-causal, head_dim 128), "i8" elsewhere;
-#   "f2": the f16 contraction software-pipelined by two key tiles (csrc/int8_attn_fwd_f2.hip) where
-#         it applies (non-causal), "f16" elsewhere.
-# Same P_i8, scales and tolerance in every mode; QATTN_INT8_PV selects the default.
-PV_MODES = ("i8", "f16", "rs", "f2")
+#   "f16": v_mfma_f32_32x32x16_f16 on f16(P_i8 * sp) x f16(v_i8 * sv), the tile scale in the operands.
+# Same P_i8, scales and tolerance in both modes; QATTN_INT8_PV selects the default.  (The role-split
+# "rs" and two-tile "f2" forms of the f16 mode measured slower and were removed in round 4.)
+PV_MODES = ("i8", "f16")
 PV_MODE = os.environ.get("QATTN_INT8_PV", "i8")
 
 
@@ -90,10 +87,6 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     v = v.to(torch.float16).contiguous()
     B, H, S, D = q.shape
     Hkv, Sk = k.shape[1], k.shape[2]
-    if pv == "rs" and (causal or D != 128):
-        pv = "i8"
-    if pv == "f2" and causal:
-        pv = "f16"
     N = B * H * S
     Nkv = B * Hkv * Sk
     dev = q.device
@@ -121,17 +114,7 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
               _lib.ptr(k_mean), Nkv, Sk, D, st)
     qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
-    if pv == "rs":
-        _lib.call("qattn_int8_quant_vop", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), Nkv,
-                  D, st)
-        _lib.call("qattn_int8_attn_fwd_rs", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
-                  _lib.ptr(vop), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, D, qks, st)
-    elif pv == "f2":
-        _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), None,
-                  Nkv, Sk, D, st)
-        _lib.call("qattn_int8_attn_fwd_f2", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
-                  _lib.ptr(vop), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, D, qks, st)
-    elif pv == "f16":
+    if pv == "f16":
         _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), None,
                   Nkv, Sk, D, st)
         _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),

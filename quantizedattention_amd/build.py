@@ -39,9 +39,6 @@ FILE_FLAGS = {
     # loop iteration for the (rare) rescale; the VGPR form keeps them in VGPRs and moves the Q
     # fragments to AGPRs instead (287 instead of 534 vector instructions per 64 keys).
     "jvp_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-    # The role-split int8 forward's softmax waves take packed f16 maxima of LDS-loaded scores: with
-    # IEEE mode off (no NaN reaches them) v_pk_max_f16 needs no canonicalising copies.
-    "int8_attn_fwd_rs.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"],
 }
 
 

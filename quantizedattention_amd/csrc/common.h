@@ -316,16 +316,6 @@ QA_DEVICE void biased_to_f16x16(const v16i& acc, float c, float nb, v2h* d) {
     d[j] = __builtin_convertvector(__builtin_elementwise_fma(a, c2, n2), v2h);
   }
 }
-// The same values with scalar v_fma_f32 (two per pair) and v_cvt_pk_f16_f32: packed fp32 issues
-// through the matrix pipe and serialises with the MFMAs of the wave's SIMD (tools/ubench/mix.py:
-// ~5 cycles of matrix pipe per v_pk_fma_f32, additive with the MFMAs; scalar fma overlaps them).
-// (Build with -fno-slp-vectorize, or the vectoriser re-packs the pairs.)
-QA_DEVICE void biased_to_f16x16_scalar(const v16i& acc, float c, float nb, v2h* d) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-    d[j] = __builtin_bit_cast(v2h, pk_f16(__builtin_fmaf(__int_as_float(acc[2 * j]), c, nb),
-                                          __builtin_fmaf(__int_as_float(acc[2 * j + 1]), c, nb)));
-}
 QA_DEVICE _Float16 biased_to_f16(int a, float c, float nb) {
   return (_Float16)__builtin_fmaf(__int_as_float(a), c, nb);
 }

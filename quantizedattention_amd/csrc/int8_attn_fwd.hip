@@ -88,24 +88,7 @@ constexpr int fwd_wps() { return CAUSAL ? 2 : Int8FwdCfg<D, PV>::WPS; }
 #ifndef QA_FWD_STAMP
 #define QA_FWD_STAMP 0
 #endif
-// Timing-only ablation builds (-DQA_FWD_ABL=<mask>, tools/ab_build.sh; results are WRONG): 1 no P.V
-// dequantisation, 2 no exponentials, 4 DMA of even tiles only, 8 no P.V MFMAs, 16 no S conversion,
-// 32 no row sum, 64 no P_i8 computation.
-#ifndef QA_FWD_ABL
-#define QA_FWD_ABL 0
-#endif
-#ifndef QA_FWD_S_SCALAR
-#define QA_FWD_S_SCALAR 0
-#endif
-#ifndef QA_FWD_DQ_SCALAR
-#define QA_FWD_DQ_SCALAR 0
-#endif
-#ifndef QA_FWD_QK2
-#define QA_FWD_QK2 0
-#endif
-#ifndef QA_FWD_UNROLL
-#define QA_FWD_UNROLL 1
-#endif
+
 #if QA_FWD_STAMP
 __device__ unsigned long long g_fwd_stamp[8192][4];
 #define FWD_STAMP(k)                                                                            \
@@ -147,7 +130,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   const int nk = SPLIT ? min(ks, Sk - k0) : Sk;    // its keys
   const long kv_row0 = (long)(bh / G) * Sk + k0;  // its key/value head's rows
   const int8_t* kbase = k_i8 + kv_row0 * D;
-  const void* vbase = PV != PV_I8
+  const void* vbase = PV == PV_F16
       ? (const void*)(reinterpret_cast<const _Float16*>(vop) + kv_row0 * D)
       : (const void*)(reinterpret_cast<const int8_t*>(vop) + kv_row0 * D);
   // causal: key tiles past the workgroup's last query are masked for all of its rows
@@ -190,7 +173,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   // lane-constant LDS byte offsets: K A-operand chunk (2s+h) of key row c32; PV_F16: V^T A-operand
   // of d-block b: key rows 4h + (i16>>2) (+16 per k-step, +8 for the 2nd read), columns
   // 32b + 16gg + 4(i16&3); PV_I8: piece b of the vt image, 16 B per lane
-  int koff[C::NKS], voff[PV == PV_F16OP ? 2 * C::NDB : C::NDB];
+  int koff[C::NKS], voff[C::NDB];
 #pragma unroll
   for (int s = 0; s < C::NKS; ++s) koff[s] = c32 * D + 16 * ((2 * s + h) ^ k_sw<D>(c32));
   if constexpr (PV == PV_F16) {
@@ -201,9 +184,6 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
       voff[b] = C::K_BYTES + key_a * 2 * D + 16 * ((d / 8) ^ v_sw<D>(key_a)) + (d % 8) * 2;
     }
-  } else if constexpr (PV == PV_F16OP) {   // piece s NDB + b of the vpo image: k-step s, d block b
-#pragma unroll
-    for (int p = 0; p < 2 * C::NDB; ++p) voff[p] = C::K_BYTES + p * 1024 + 16 * lane;
   } else {
 #pragma unroll
     for (int b = 0; b < C::NDB; ++b) voff[b] = C::K_BYTES + b * 1024 + 16 * lane;
@@ -275,12 +255,6 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       const float nb = -KMAG * c;
 #if QA_FWD_S_PK
       rm = biased_to_f16(mx, c, nb);
-      if constexpr (PV == PV_F16OP || QA_FWD_S_SCALAR) {   // scalar f32 (no packed fp32)
-        biased_to_f16x16_scalar(acc, c, nb, s2);
-      } else if constexpr ((QA_FWD_ABL & 16) != 0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s2[j] = __builtin_bit_cast(v2h, acc[2 * j] ^ acc[2 * j + 1]);
-      } else
       biased_to_f16x16(acc, c, nb, s2);
 #else
       rm = fma_mix1(__int_as_float(mx), c, nb);
@@ -350,20 +324,13 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   // second half: e = exp2(d) (sm2_exp), then l += er * sum e and the P operand (sm2)
   //   PV_F16: f16(P_i8 * sp) as 2 x 4 packed dwords; PV_I8: the 16 P_i8 bytes
   auto sm2_exp = [&](const SmTile& st, v2h* e) {
-    if constexpr ((QA_FWD_ABL & 2) != 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) e[j] = st.d[j];
-      return;
-    }
     exp2_pk4(&st.d[0], &e[0]);
     exp2_pk4(&st.d[4], &e[4]);
   };
   auto sm2 = [&](const SmTile& st, const v2h* e, v4u* pw) {
     // row sum of e: packed f16 adds (pairs, then sums of 4 and 8 values <= 8), one f32 mix-add
-    if constexpr ((QA_FWD_ABL & 32) == 0) {
-      const v2h s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
-      l = fmaf(pk_hsum(s), st.er, l);
-    }
+    const v2h s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+    l = fmaf(pk_hsum(s), st.er, l);
     if ((CAUSAL || QA_FWD_LITERAL_P) && st.diag) {   // the literal-chain P_i8 of the tile (sm1)
       if constexpr (PV != PV_I8) {
         const _Float16 sp = (_Float16)st.cpv;
@@ -393,11 +360,6 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     } else {
       const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
       unsigned y[8];
-      if constexpr ((QA_FWD_ABL & 64) != 0) {
-        pw[0] = v4u{__builtin_bit_cast(unsigned, e[0]), __builtin_bit_cast(unsigned, e[3]),
-                    __builtin_bit_cast(unsigned, e[5]), __builtin_bit_cast(unsigned, e[7])};
-        return;
-      }
       p_index8(e, k127, y);
       pw[0] = __builtin_bit_cast(v4u, pack_p_index(y));
     }
@@ -417,9 +379,6 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
           const char* a = vl + voff[b] + 16 * s * 2 * D;
           va[s * C::NDB + b] = __builtin_bit_cast(v8h, ds_read_tr16_x2(a, a + 8 * 2 * D));
         }
-    } else if constexpr (PV == PV_F16OP) {
-#pragma unroll
-      for (int p = 0; p < 2 * C::NDB; ++p) va[p] = *reinterpret_cast<const v8h*>(vl + voff[p]);
     } else {
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b) va[b] = *reinterpret_cast<const v4i*>(vl + voff[b]);
@@ -435,11 +394,6 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
           o[b] = mfma_f16(va[s * C::NDB + b], __builtin_bit_cast(v8h, pw[s]), o[b]);
     } else {
       const v4i p = __builtin_bit_cast(v4i, pw[0]);
-      if constexpr ((QA_FWD_ABL & 8) != 0) {
-#pragma unroll
-        for (int b = 0; b < C::NDB; ++b) pacc[b] = kmag + v16i{p[0], p[1], p[2], p[3], va[b][0]};
-        return;
-      }
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b) pacc[b] = mfma_i8(va[b], p, kmag);
     }
@@ -447,27 +401,17 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   // PV_I8: O += (KMAG + X) * (sp * sv) for the tile's exact int32 X (one fused op per element)
   auto pv_dequant = [&](float cpv) {
     if constexpr (PV == PV_I8) {
-      if constexpr ((QA_FWD_ABL & 1) != 0) {
+      // explicit v_pk_fma_f32 pairs (scalar v_fma_f32 measured 2-3 % slower)
+      const v2f_ c2 = {cpv, cpv};
 #pragma unroll
-        for (int b = 0; b < C::NDB; ++b) o[b][b] += __int_as_float(pacc[b][0]);
-      } else {
+      for (int b = 0; b < C::NDB; ++b)
 #pragma unroll
-        for (int b = 0; b < C::NDB; ++b) {
-          if (b < QA_FWD_DQ_SCALAR) {   // scalar v_fma_f32 (the file is built without SLP)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[b][r] = fmaf(__int_as_float(pacc[b][r]), cpv, o[b][r]);
-          } else {   // explicit v_pk_fma_f32 pairs
-            const v2f_ c2 = {cpv, cpv};
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-              const v2f_ a = {__int_as_float(pacc[b][r]), __int_as_float(pacc[b][r + 1])};
-              const v2f_ y = __builtin_elementwise_fma(a, c2, v2f_{o[b][r], o[b][r + 1]});
-              o[b][r] = y[0];
-              o[b][r + 1] = y[1];
-            }
-          }
+        for (int r = 0; r < 16; r += 2) {
+          const v2f_ a = {__int_as_float(pacc[b][r]), __int_as_float(pacc[b][r + 1])};
+          const v2f_ y = __builtin_elementwise_fma(a, c2, v2f_{o[b][r], o[b][r + 1]});
+          o[b][r] = y[0];
+          o[b][r + 1] = y[1];
         }
-      }
       obias += cpv;
     }
   };
@@ -482,78 +426,58 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   // (its row max cannot move m) and it keeps the loop body branch-free.
   //   cur, nxt: ring slots of tiles t and t+1; fill: the slot the DMA of tile t+3 goes to (freed by
   //   the barrier); ckn, svqn: the scales of tile t+1
-  // QA_FWD_QK2: QK^T runs two tiles ahead (QK(t+2) in iteration t, held in nacc1 across one
-  // iteration), so SM1(t+1) never waits on an MFMA of its own iteration, and P.V(t) is issued ahead
-  // of QK(t+2) so that its product has drained when the dequantisation after SM1 reads it.  The
-  // barrier then needs tile t+2 landed (the DMA of tile t+3 stays in flight).
-  v16i nacc1;
+  // One loop iteration per tile t: SM2 and P.V of tile t, QK and SM1 of tile t+1.  The last iteration
+  // computes QK / SM1 of a duplicate of the last tile (its slot holds a clamped re-load): harmless
+  // (its row max cannot move m) and it keeps the loop body branch-free.
+  //   cur, nxt: ring slots of tiles t and t+1; fill: the slot the DMA of tile t+3 goes to (freed by
+  //   the barrier); ckn, svqn: the scales of tile t+1
   auto iter = [&](int t, int cur, int nxt, int fill, float ckn, float svqn) {
-    ring_wait_barrier<QA_FWD_QK2 ? 0 : C::IPW>();   // tiles <= t+1 (QK2: t+2) landed; `fill` free
-    if ((QA_FWD_ABL & 4) == 0 || (t & 1) == 0)
-      dma.issue(smem_lds + fill * C::SLOT, min(t + 3, nt - 1));
+    ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot `fill` is free
+    dma.issue(smem_lds + fill * C::SLOT, min(t + 3, nt - 1));
+    // Phase order (pinned: hipcc otherwise issues the QK(t+1) chain right before its consumer
+    // SM1(t+1) and the wave stalls on it): fragment reads, the 16 exponentials of tile t (which
+    // cover the LDS latency), QK(t+1), then the rest of SM2(t), PV(t) and SM1(t+1).
     const int tn = min(t + 1, nt - 1);
     v4i kf[C::NKS];
-    qk_load(nxt, kf);   // K of tile t+1 (QK2: t+2)
+    qk_load(nxt, kf);
     VFrag va[NVF];
     pv_load(cur, va);
     v2h e[8];
     sm2_exp(st, e);
-    if constexpr (QA_FWD_QK2) {
-      v4u pw[2];
-      sm2(st, e, pw);
-      cpv_pend = st.cpv;
-      pv_mma(va, pw);
-      __builtin_amdgcn_sched_barrier(0);
-      const v16i nacc2 = qk_mma(kf);
-      __builtin_amdgcn_sched_barrier(0);
-      sm1(nacc1, tn, st, ckn, svqn);   // (may rescale O, obias and cpv_pend)
-      pv_dequant(cpv_pend);
-      nacc1 = nacc2;
-    } else {
-      // Phase order (pinned: hipcc otherwise issues the QK(t+1) chain right before its consumer
-      // SM1(t+1) and the wave stalls on it): fragment reads, the 16 exponentials of tile t (which
-      // cover the LDS latency), QK(t+1), then the rest of SM2(t), PV(t) and SM1(t+1).
-      __builtin_amdgcn_sched_barrier(0);
-      const v16i nacc = qk_mma(kf);
-      __builtin_amdgcn_sched_barrier(0);
-      v4u pw[2];
-      sm2(st, e, pw);
-      cpv_pend = st.cpv;
-      pv_mma(va, pw);
-      sm1(nacc, tn, st, ckn, svqn);   // (may rescale O, obias and cpv_pend)
-      pv_dequant(cpv_pend);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
-    }
+    __builtin_amdgcn_sched_barrier(0);
+    const v16i nacc = qk_mma(kf);
+    __builtin_amdgcn_sched_barrier(0);
+    v4u pw[2];
+    sm2(st, e, pw);
+    cpv_pend = st.cpv;
+    pv_mma(va, pw);
+    sm1(nacc, tn, st, ckn, svqn);   // (may rescale O, obias and cpv_pend)
+    pv_dequant(cpv_pend);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
   };
-  constexpr int QKA = QA_FWD_QK2 ? 2 : 1;   // QK runs this many tiles ahead of P.V
   if (active) {
     {
       v4i kf[C::NKS];
       qk_load(0, kf);
       sm1(qk_mma(kf), 0, st, ck0, svq0);
-      if constexpr (QA_FWD_QK2) {
-        qk_load(1, kf);   // (tile min(1, nt - 1): the prologue's DMA clamps it)
-        nacc1 = qk_mma(kf);
-      }
     }
     // groups of NSLOT = 4 tiles with compile-time ring slots (immediate LDS offsets, one 16-B read
     // of each scale table per group), then the remaining tiles with run-time slots
     static_assert(C::NSLOT == 4, "ring of 4 slots");
     int t = 0;
-    for (; QA_FWD_UNROLL && t + 4 <= nt; t += 4) {
+    for (; t + 4 <= nt; t += 4) {
       const v4f ck4 = *reinterpret_cast<const v4f*>(ck_lds + t);
       const v4f sv4 = PV == PV_I8 ? *reinterpret_cast<const v4f*>(svq_lds + t) : v4f{};
-      iter(t, 0, QKA & 3, 3, ck4[0], sv4[0]);
-      iter(t + 1, 1, (1 + QKA) & 3, 0, ck4[1], sv4[1]);
-      iter(t + 2, 2, (2 + QKA) & 3, 1, ck4[2], sv4[2]);
-      iter(t + 3, 3, (3 + QKA) & 3, 2, ck4[3], sv4[3]);
+      iter(t, 0, 1, 3, ck4[0], sv4[0]);
+      iter(t + 1, 1, 2, 0, ck4[1], sv4[1]);
+      iter(t + 2, 2, 3, 1, ck4[2], sv4[2]);
+      iter(t + 3, 3, 0, 2, ck4[3], sv4[3]);
     }
     for (; t < nt; ++t)
-      iter(t, t & 3, (t + QKA) & 3, (t + 3) & 3, ck_lds[t], PV == PV_I8 ? svq_lds[t] : 0.f);
+      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], PV == PV_I8 ? svq_lds[t] : 0.f);
   } else {   // a wave past the last query row: the barriers and the ring's DMA only
     for (int t = 0; t < nt; ++t) {
-      ring_wait_barrier<QA_FWD_QK2 ? 0 : C::IPW>();
-      if ((QA_FWD_ABL & 4) == 0 || (t & 1) == 0)
-        dma.issue(smem_lds + ((t + 3) & 3) * C::SLOT, min(t + 3, nt - 1));
+      ring_wait_barrier<C::IPW>();
+      dma.issue(smem_lds + ((t + 3) & 3) * C::SLOT, min(t + 3, nt - 1));
     }
   }
   vmcnt_wait_all();
@@ -590,7 +514,6 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
   using C = Int8FwdCfg<D, PV>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int lds = C::RING + (int)((((sk_tok / 32) + 3) / 4 * 4) * 4 * (PV == PV_I8 ? 2 : 1));
-  static_assert(PV != PV_F16OP || D == 128 || D == 64, "head dims");
   { static int granted_ = 0; lds_grant((const void*)int8_attn_fwd_kernel<D, PV, CAUSAL>, lds, granted_); }
   hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV, CAUSAL>), dim3((unsigned)(nq * bh)),
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
@@ -691,14 +614,6 @@ extern "C" int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const vo
                                       float qks, void* stream) {
   return fwd_dispatch<PV_F16>(q_i8, sq, k_i8, sk, vdq, nullptr, out, lse, bh, sq_tok, sk_tok, group,
                               causal, head_dim, qks, stream);
-}
-
-extern "C" int qattn_int8_attn_fwd_vpo_ex(const void* q_i8, const void* sq, const void* k_i8,
-                                          const void* sk, const void* vpo, void* out, void* lse,
-                                          long bh, long sq_tok, long sk_tok, int group, int causal,
-                                          int head_dim, float qks, void* stream) {
-  return fwd_dispatch<PV_F16OP>(q_i8, sq, k_i8, sk, vpo, nullptr, out, lse, bh, sq_tok, sk_tok, group,
-                                causal, head_dim, qks, stream);
 }
 
 extern "C" int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,

@@ -1,13 +1,11 @@
-// Shared pieces of the int8 attention forwards (int8_attn_fwd.hip: the mixed-wave kernel;
-// int8_attn_fwd_rs.hip: the role-split kernel): tile configuration, K / V swizzles, and the LDS-DMA
-// plan of one 32-key tile.
+// Tile configuration, K / V swizzles and the LDS-DMA plan of one 32-key tile of the int8 attention
+// forward (int8_attn_fwd.hip).
 #pragma once
 #include "common.h"
 
 namespace qattn {
 
-// PV_F16OP: the f16 contraction (as PV_F16) on the operand-order image of qattn_int8_quant_vpo
-enum PvMode { PV_F16 = 0, PV_I8 = 1, PV_F16OP = 2 };
+enum PvMode { PV_F16 = 0, PV_I8 = 1 };
 
 // A/B knobs (tools/ab_build.sh, tools/ab_time.py; measured on MI355X):
 //   QA_FWD_WAVES    waves (32 query rows each) per workgroup.  8 halve the L2 -> LDS bytes per
@@ -49,7 +47,7 @@ struct Int8FwdCfg {
   static constexpr int KT = 32;                 // keys per tile / ring slot
   static constexpr int NSLOT = 4;               // ring slots
   static constexpr int K_BYTES = KT * D;        // int8 K tile
-  static constexpr int V_BYTES = PV != PV_I8 ? KT * D * 2 : KT * D;   // f16 vdq / i8 V^T image
+  static constexpr int V_BYTES = PV == PV_F16 ? KT * D * 2 : KT * D;   // f16 vdq / i8 V^T image
   static constexpr int SLOT = K_BYTES + V_BYTES;
   static constexpr int NKS = D / 32;            // i8 k-steps for QK^T
   static constexpr int NDB = D / 32;            // 32-wide d blocks of O^T
@@ -64,7 +62,7 @@ struct Int8FwdCfg {
   // waves per SIMD the register budget must allow (__launch_bounds__ second argument): two (<= 256
   // VGPRs), three for the PV_F16 kernel at QA_FWD_OCC_F16 = 3 with 4-wave workgroups
   static constexpr int WPS = (PV == PV_F16 && WAVES == 4) ? QA_FWD_OCC_F16 : 2;
-  static constexpr bool QK_BIAS = QA_FWD_QK_BIAS < 0 ? PV != PV_F16 : QA_FWD_QK_BIAS != 0;
+  static constexpr bool QK_BIAS = QA_FWD_QK_BIAS < 0 ? PV == PV_I8 : QA_FWD_QK_BIAS != 0;
   // the ring, reused as the output staging area of the epilogue
   static constexpr int STAGE = WAVES * RowTile<D, _Float16>::BYTES;
   static constexpr int RING = NSLOT * SLOT > STAGE ? NSLOT * SLOT : STAGE;
@@ -116,12 +114,12 @@ struct DmaPlan {
         lds_off[i] = C::K_BYTES + vi * 1024;
         stride[i] = C::V_BYTES;
         rsrc[i] = make_rsrc(vbase, (unsigned)S * 2 * D);
-      } else {   // PV_I8 / PV_F16OP: an operand-order image, plain 1-KiB pieces
+      } else {   // PV_I8: the operand-order vt image, plain 1-KiB pieces
         const int vi = inst - C::K_INST;
         voff[i] = vi * 1024 + 16 * lane;
         lds_off[i] = C::K_BYTES + vi * 1024;
         stride[i] = C::V_BYTES;
-        rsrc[i] = make_rsrc(vbase, (unsigned)S * (C::V_BYTES / C::KT));
+        rsrc[i] = make_rsrc(vbase, (unsigned)S * D);
       }
     }
   }

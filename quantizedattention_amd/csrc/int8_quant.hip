@@ -118,77 +118,6 @@ __global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restric
     *reinterpret_cast<v4i*>(vt + blk * 32 * D + b * 1024 + 16 * lane) = pack_acc_bytes(t);
   }
 }
-// ------------------------------------------------------------ V with the f16 P.V operand image
-// One wave per 32-row block of v: the reference quantiser (v_i8 row-major + sv, bit-exact as above)
-// and the role-split forward's P.V operand image of vdq = f16(v_i8 * sv) (int8_attn_fwd_rs.hip):
-// per block 2 D/32 pieces of 1 KiB; piece 4 s2 + b (b < D/32) holds for lane L = 32h + i the 8
-// halves vdq[key 16 s2 + 8h + j][32b + i], j = 0..7 -- the A operand of v_mfma_f32_32x32x16_f16
-// for V^T, keys in natural order.  The block's vdq goes through a swizzled row-major LDS image and
-// comes back transposed by ds_read_b64_tr_b16 (two reads of 4 keys per operand).
-// PERM: the keys of each 16-key k-step in the order of the S^T accumulator of the mixed-wave forward
-// (common.h: slot j of half h holds key 8(j >> 2) + 4h + (j & 3)), so that the accumulator's f16 P
-// operand needs no reordering (qattn_int8_quant_vpo, the f16 P.V mode of int8_attn_fwd.hip).
-template <int D, bool PERM = false>
-__global__ __launch_bounds__(256) void quant_vop_kernel(const _Float16* __restrict__ v,
-                                                        int8_t* __restrict__ vi,
-                                                        _Float16* __restrict__ sv,
-                                                        _Float16* __restrict__ vop, long nblocks) {
-  constexpr int ELEMS = 32 * D;
-  constexpr int ITERS = ELEMS / 512;
-  constexpr int NDB = D / 32;
-  constexpr int CH = D / 8;                    // 16-B chunks per f16 row
-  __shared__ __attribute__((aligned(16))) char img[4][32 * D * 2];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long blk = (long)blockIdx.x * 4 + w;
-  const bool live = blk < nblocks;
-  char* im = img[w];
-  auto sw = [](int key) { return (key & 3) << ((D == 128) ? 2 : 1); };
-  if (live) {
-    const _Float16* xb = v + blk * ELEMS;
-    v8h x[ITERS];
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      x[i] = *reinterpret_cast<const v8h*>(xb + (i * 64 + lane) * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf((float)x[i][j]));
-    }
-    amax = wave_max_f(amax);
-    const _Float16 s16 = (_Float16)(amax / 127.0f);
-    const float s = (float)s16;
-    const float r = quant_rcp(s);
-    if (lane == 0) sv[blk] = s16;
-#pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const int e = (i * 64 + lane) * 8;
-      unsigned lo, hi;
-      float qf[8];
-      quant8(x[i], s, r, lo, hi, qf);
-      *reinterpret_cast<v2u*>(vi + blk * ELEMS + e) = v2u{lo, hi};
-      v8h dq;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dq[j] = (_Float16)(qf[j] * s);
-      const int key = e / D, c = (e % D) / 8;
-      *reinterpret_cast<v8h*>(im + key * 2 * D + 16 * (c ^ sw(key))) = dq;
-    }
-  }
-  __syncthreads();
-  if (!live) return;
-  const int h = lane >> 5, gg = (lane >> 4) & 1, i16 = lane & 15;
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int b = 0; b < NDB; ++b) {
-      const int key = 16 * s2 + (PERM ? 4 : 8) * h + (i16 >> 2);
-      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
-      const char* a = im + key * 2 * D + 16 * ((d / 8) ^ sw(key)) + (d % 8) * 2;
-      const v8s t = ds_read_tr16_x2(a, a + (PERM ? 8 : 4) * 2 * D);
-      *reinterpret_cast<v8s*>(reinterpret_cast<char*>(vop) + blk * ELEMS * 2 + (s2 * NDB + b) * 1024 +
-                              16 * lane) = t;
-    }
-  (void)CH;
-}
-
 // vt from stored indices (an int8 key/value cache restored from its wire format, kv_cache.py)
 template <int D>
 __global__ __launch_bounds__(256) void v_image_kernel(const int8_t* __restrict__ vi,
@@ -302,38 +231,6 @@ extern "C" int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt
   else
     hipLaunchKernelGGL(quant_vt_kernel<64>, grid, block, 0, st, (const _Float16*)v, (int8_t*)v_i8,
                        (_Float16*)sv, (int8_t*)vt, nblocks);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
-extern "C" int qattn_int8_quant_vop(const void* v, void* v_i8, void* sv, void* vop, long rows,
-                                    int head_dim, void* stream) {
-  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  const long nblocks = rows / 32;
-  if (nblocks == 0) return 0;
-  dim3 grid((unsigned)((nblocks + 3) / 4)), block(256);
-  hipStream_t st = (hipStream_t)stream;
-  if (head_dim == 128)
-    hipLaunchKernelGGL(quant_vop_kernel<128>, grid, block, 0, st, (const _Float16*)v, (int8_t*)v_i8,
-                       (_Float16*)sv, (_Float16*)vop, nblocks);
-  else
-    hipLaunchKernelGGL(quant_vop_kernel<64>, grid, block, 0, st, (const _Float16*)v, (int8_t*)v_i8,
-                       (_Float16*)sv, (_Float16*)vop, nblocks);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
-extern "C" int qattn_int8_quant_vpo(const void* v, void* v_i8, void* sv, void* vpo, long rows,
-                                    int head_dim, void* stream) {
-  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  const long nblocks = rows / 32;
-  if (nblocks == 0) return 0;
-  dim3 grid((unsigned)((nblocks + 3) / 4)), block(256);
-  hipStream_t st = (hipStream_t)stream;
-  if (head_dim == 128)
-    hipLaunchKernelGGL((quant_vop_kernel<128, true>), grid, block, 0, st, (const _Float16*)v,
-                       (int8_t*)v_i8, (_Float16*)sv, (_Float16*)vpo, nblocks);
-  else
-    hipLaunchKernelGGL((quant_vop_kernel<64, true>), grid, block, 0, st, (const _Float16*)v,
-                       (int8_t*)v_i8, (_Float16*)sv, (_Float16*)vpo, nblocks);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -112,9 +112,8 @@ void check_int8(const Tensor& q, const Tensor& k, const Tensor& v) {
 
 using T8 = std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor>;
 
-// attention_int8._int8_forward.  pv: the P.V mode, as attention_int8.PV_MODES ("i8", "f16", "rs",
-// "f2"; ops.int8_fwd passes attention_int8.PV_MODE); "" = QATTN_INT8_PV, else "i8".  "rs" runs as
-// "i8" where the role-split kernel does not apply (causal, head_dim 64), "f2" as "f16" when causal.
+// attention_int8._int8_forward.  pv: the P.V mode, as attention_int8.PV_MODES ("i8", "f16";
+// ops.int8_fwd passes attention_int8.PV_MODE); "" = QATTN_INT8_PV, else "i8".
 T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smooth, bool causal,
             c10::string_view pv_in) {
   check_int8(q_in, k_in, v_in);
@@ -129,10 +128,8 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
     const char* e = std::getenv("QATTN_INT8_PV");
     pv = (e && *e) ? e : "i8";
   }
-  TORCH_CHECK_VALUE(pv == "i8" || pv == "f16" || pv == "rs" || pv == "f2", "qattn int8: unknown P.V mode '",
-                    pv, "' (one of i8, f16, rs, f2)");
-  if (pv == "rs" && (causal || D != 128)) pv = "i8";
-  if (pv == "f2" && causal) pv = "f16";
+  TORCH_CHECK_VALUE(pv == "i8" || pv == "f16", "qattn int8: unknown P.V mode '", pv,
+                    "' (one of i8, f16)");
   const bool f16pv = pv != "i8";
   Tensor q_i8 = empty({N, D}, at::kChar, q), k_i8 = empty({Nkv, D}, at::kChar, q),
          v_i8 = empty({Nkv, D}, at::kChar, q);
@@ -156,18 +153,7 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
                             c.stream),
        "quantise k");
   const float qks = qk_scale(D);
-  if (pv == "rs") {
-    call(qattn_int8_quant_vop(P(v), P(v_i8), P(sv), P(vop), Nkv, (int)D, c.stream), "quantise v");
-    call(qattn_int8_attn_fwd_rs(P(q_i8), P(sq), P(k_i8), P(sk), P(vop), P(O), P(lse), B * H, S, Sk,
-                                (int)(H / Hkv), (int)D, qks, c.stream),
-         "int8 forward");
-  } else if (pv == "f2") {
-    call(qattn_int8_quant(P(v), P(v_i8), P(sv), P(vop), nullptr, Nkv, (int)Sk, (int)D, c.stream),
-         "quantise v");
-    call(qattn_int8_attn_fwd_f2(P(q_i8), P(sq), P(k_i8), P(sk), P(vop), P(O), P(lse), B * H, S, Sk,
-                                (int)(H / Hkv), (int)D, qks, c.stream),
-         "int8 forward");
-  } else if (f16pv) {
+  if (f16pv) {
     call(qattn_int8_quant(P(v), P(v_i8), P(sv), P(vop), nullptr, Nkv, (int)Sk, (int)D, c.stream),
          "quantise v");
     call(qattn_int8_attn_fwd_ex(P(q_i8), P(sq), P(k_i8), P(sk), P(vop), P(O), P(lse), B * H, S, Sk,

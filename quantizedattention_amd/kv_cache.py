@@ -92,8 +92,7 @@ class QuantizedKV:
         return self._vt
 
     def operand(self, pv: str) -> torch.Tensor:
-        """The P.V operand of mode ``pv`` ("f16": f16(v_i8 * sv); "i8" / "rs": the int8 V^T image --
-        the role-split forward is a training-shape kernel, a cache runs the int8 decoding path)."""
+        """The P.V operand of mode ``pv`` ("f16": f16(v_i8 * sv); "i8": the int8 V^T image)."""
         return self.vdq() if _pv_mode(pv) == "f16" else self.vt()
 
     def drop_operands(self) -> None:
@@ -219,8 +218,7 @@ def _pv_mode(pv):
     pv = attention_int8.PV_MODE if pv is None else pv
     if pv not in attention_int8.PV_MODES:
         raise _lib.QAttnError(f"qattn kv cache: unknown P.V mode {pv!r} (one of {attention_int8.PV_MODES})")
-    # the training-shape schedules run as their contraction's cache path
-    return {"rs": "i8", "f2": "f16"}.get(pv, pv)
+    return pv
 
 
 def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False, pv=None):
@@ -230,7 +228,7 @@ def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False
     are the LAST Sq positions (query i keeps keys <= Sk - Sq + i), Sq <= Sk.  Returns (O fp16
     [B, Hq, Sq, D], lse fp16 [B*Hq*Sq]); without ``causal`` identical to the forward on the un-cached
     tensors (bit-identical when one key split covers the cache).  ``pv``: the P.V mode (default
-    attention_int8.PV_MODE; "rs" runs as "i8" and "f2" as "f16" here).
+    attention_int8.PV_MODE).
     Non-causal with the int8 P.V at head_dim 128 runs in the decoding layout (_decode_split: the
     grouped query heads of a key/value head in one workgroup, long caches split over the keys and
     merged); the results equal the one-pass forward's up to the merge's rounding (<= 2e-3).

@@ -20,7 +20,7 @@ SHAPES = [(1, 4, 2, 128, 96, 64), (2, 4, 1, 64, 160, 128), (1, 2, 2, 160, 128, 1
           (1, 2, 2, 128, 128, 64)]
 
 
-@pytest.fixture(params=["f16", "i8", "f2"])
+@pytest.fixture(params=["f16", "i8"])
 def pv(request, monkeypatch):
     from quantizedattention_amd import attention_int8
     monkeypatch.setattr(attention_int8, "PV_MODE", request.param)

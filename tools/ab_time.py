@@ -53,10 +53,6 @@ call("qattn_int8_quant", P(k), P(ki), P(sk), None, None, N, S, D, st)
 call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 if entry("qattn_int8_quant_vt") is not None:
     call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
-vpo = None
-if entry("qattn_int8_quant_vpo") is not None:
-    vpo = e(N, D, dt=torch.float16)
-    call("qattn_int8_quant_vpo", P(v), P(vi), P(sv), P(vpo), N, D, st)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
 fns = {}
 if entry("qattn_int8_attn_fwd_ex") is not None:
@@ -65,12 +61,6 @@ if entry("qattn_int8_attn_fwd_ex") is not None:
 if entry("qattn_int8_attn_fwd_i8pv_ex") is not None:
     fns["i8"] = lambda: call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv),
                              P(O), P(lse), B * H, S, S, 1, int(causal), D, qks, st)
-if entry("qattn_int8_attn_fwd_vpo_ex") is not None:
-    fns["vpo"] = lambda: call("qattn_int8_attn_fwd_vpo_ex", P(qi), P(sq), P(ki), P(sk), P(vpo), P(O), P(lse),
-                              B * H, S, S, 1, int(causal), D, qks, st)
-if entry("qattn_int8_attn_fwd_f2") is not None and not causal:
-    fns["f2"] = lambda: call("qattn_int8_attn_fwd_f2", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse),
-                             B * H, S, S, 1, D, qks, st)
 only = os.environ.get("QATTN_AB_MODES")
 if only:
     fns = {k_: f_ for k_, f_ in fns.items() if k_ in only.split(",")}

@@ -1,6 +1,6 @@
 """Launch one kernel of the int8 / bf16 paths N times at the headline shape (for rocprofv3 passes).
 
-    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd (f16 P.V), int8_fwd_i8 (default), int8_fwd_rs (role split), int8_fwd_f2 (two-tile pipeline), int8_dkdv, int8_dv, int8_dk, int8_dq, int8_all, bf16_fwd,
+    python tools/kernel_runner.py <name> [reps]   name in: int8_fwd (f16 P.V), int8_fwd_i8 (default), int8_dkdv, int8_dv, int8_dk, int8_dq, int8_all, bf16_fwd,
                                                            bf16_bwd, jvp, quant
 """
 import math
@@ -37,8 +37,6 @@ vdq = torch.empty((N, D), dtype=torch.float16, device="cuda")
 _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 vt = torch.empty((N, D), dtype=torch.int8, device="cuda")
 _lib.call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
-vop = torch.empty((N, D), dtype=torch.float16, device="cuda")
-_lib.call("qattn_int8_quant_vop", P(v), P(vi), P(sv), P(vop), N, D, st)
 dOi = torch.empty((N, D), dtype=torch.int8, device="cuda")
 sdO = torch.empty((N // 32,), dtype=torch.float16, device="cuda")
 LD = torch.empty((N, 2), dtype=torch.float32, device="cuda")
@@ -60,12 +58,6 @@ for name in [n for _ in range(reps) for n in names]:
     elif name == "int8_fwd_i8":
         _lib.call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv), P(O), P(lse),
                   B * H, S, S, 1, 0, D, qks, st)
-    elif name == "int8_fwd_f2":
-        _lib.call("qattn_int8_attn_fwd_f2", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse), B * H, S, S, 1, D,
-                  qks, st)
-    elif name == "int8_fwd_rs":
-        _lib.call("qattn_int8_attn_fwd_rs", P(qi), P(sq), P(ki), P(sk), P(vop), P(O), P(lse), B * H, S, S, 1, D,
-                  qks, st)
     elif name == "int8_dkdv":
         _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
                   P(qb), P(ob), P(dk), P(dv), B * H, S, D, qks, sms, st)
