@@ -461,10 +461,13 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       sm1(qk_mma(kf), 0, st, ck0, svq0);
     }
     // groups of NSLOT = 4 tiles with compile-time ring slots (immediate LDS offsets, one 16-B read
-    // of each scale table per group), then the remaining tiles with run-time slots
+    // of each scale table per group), then the remaining tiles with run-time slots.  Only where the
+    // unrolled body fits the register budget: the causal kernel (diagonal-tile masks and the literal
+    // P chain) and the 3-wave f16 P.V kernel spill with it, so they keep the run-time-slot loop.
     static_assert(C::NSLOT == 4, "ring of 4 slots");
+    constexpr bool UNROLL = PV == PV_I8 && !CAUSAL;
     int t = 0;
-    for (; t + 4 <= nt; t += 4) {
+    for (; UNROLL && t + 4 <= nt; t += 4) {
       const v4f ck4 = *reinterpret_cast<const v4f*>(ck_lds + t);
       const v4f sv4 = PV == PV_I8 ? *reinterpret_cast<const v4f*>(svq_lds + t) : v4f{};
       iter(t, 0, 1, 3, ck4[0], sv4[0]);

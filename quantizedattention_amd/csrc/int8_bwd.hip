@@ -500,8 +500,13 @@ void int8_bwd_kernel(
     }
     // key > query as one compare per score against an immediate: dd = key - (first query of the
     // lane's row group), INT_MIN off the diagonal tiles (nothing masked there)
+    // (the lane's c32 - 4h is re-derived from the lane id here, two mbcnt and two bit ops, rather
+    // than kept live: at 256 VGPRs the causal dK+dV kernels otherwise spill it and reload it from
+    // scratch on every tile)
+    const int ln = __lane_id();
+    const int lane_rel = (ln & 31) - 4 * (ln >> 5);   // c32 - 4h
     const int dd = !diag ? INT_MIN
-                         : (ROLE == ROLE_DQ ? (y0 + 4 * h) - (x0 + c32) : (x0 + c32) - (y0 + 4 * h));
+                         : (ROLE == ROLE_DQ ? (y0 - x0) - lane_rel : (x0 - y0) + lane_rel);
     if constexpr (G::HAS_LD) {
       const float* ld = reinterpret_cast<const float*>(slot(t) + G::LDO);
 #pragma unroll

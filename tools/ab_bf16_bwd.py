@@ -19,17 +19,20 @@ k = torch.randn((B, H, S, D), device="cuda", generator=g).half()
 v = torch.randn((B, H, S, D), device="cuda", generator=g).bfloat16()
 dO = torch.randn((B, H, S, D), device="cuda", generator=g)
 O, lse = A.helion_atten_bf16_fwd_training(q, k, v, causal)
-res = {}
-for entry in ("auto", "ws", "qattn_bf16_bwd_ex", "qattn_bf16_bwd_split_ex"):
+res, hs = {}, {}
+ENTRIES = os.environ.get("QATTN_AB_ENTRIES", "auto,ws,qattn_bf16_bwd_ex,qattn_bf16_bwd_split_ex").split(",")
+for entry in ENTRIES:
     A._BWD_ENTRY = entry
     ts = []
     for i in range(8):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        A.helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, causal, dO)
+        out = A.helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, causal, dO)
         b.record()
         torch.cuda.synchronize()
         if i >= 2:
             ts.append(a.elapsed_time(b))
     res[entry] = sorted(ts)[len(ts) // 2]
-print(os.environ.get("QATTN_LIB", "default"), {k: round(v, 3) for k, v in res.items()})
+    # checksum of the gradient bits (on the GPU: bit-identical outputs give equal sums)
+    hs[entry] = sum(int(t.float().view(torch.int32).to(torch.int64).sum()) * (i + 1) for i, t in enumerate(out[:3]))
+print(os.environ.get("QATTN_LIB", "default"), {k: round(v, 3) for k, v in res.items()}, hs)
