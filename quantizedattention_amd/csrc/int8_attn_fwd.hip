@@ -110,7 +110,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   FWD_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per-tile scales: ck = sk * qks (f32); PV_I8 also sv / 127 (f32)
-  float* ck_lds = reinterpret_cast<float*>(smem + C::TAB);
+  float* ck_lds = reinterpret_cast<float*>(smem + C::RING);
 
   const int nq = (Sq + C::QROWS - 1) / C::QROWS;
   int bh, qt;
@@ -163,13 +163,6 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     for (int s = 0; s < C::NKS; ++s) qf[s] = *reinterpret_cast<const v4i*>(qrow + 32 * s);
     cq = (float)sq[(head_row0 + q0) / 32];
   }
-  // C::QLDS: the fragments go to this wave's LDS pieces and are re-read per tile (wave-private:
-  // LDS accesses of one wave complete in order, no barrier)
-  char* const q_lds = smem + C::RING + (wave * C::NKS * 1024 + 16 * lane) * (C::QLDS != 0);
-  if constexpr (C::QLDS != 0) {
-#pragma unroll
-    for (int s = 0; s < C::NKS; ++s) *reinterpret_cast<v4i*>(q_lds + s * 1024) = qf[s];
-  }
   // the biased accumulator seed, opaque to the compiler (so it stays in 16 registers instead of
   // being re-materialised by 16 v_mov per use)
   v16i kmag;
@@ -207,41 +200,27 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   // PV_I8: the dequantisation factor of the tile whose P.V is in flight while SM1 of the next tile
   // runs; a running-max move there rescales it with O (its int32 product is added after SM1)
   float cpv_pend = 0.f;
-  // 3 waves per SIMD (QA_FWD_OCC_I8 = 3, <= 168 VGPRs): the P.V product of a tile in two halves of
-  // two d blocks each (32 accumulator registers instead of 64), the second half issued after the
-  // running-max update of SM1(t+1) and the first half's dequantisation, and the S conversion of
-  // SM1(t+1) after both
-  constexpr bool LATE_S = PV == PV_I8 && !CAUSAL && C::WPS == 3 && D == 128;
-  static_assert(!LATE_S || C::NDB == 4, "two halves of two d blocks");
 
   // ring slot u (the loop below passes compile-time slot numbers: LDS offsets become immediates)
   auto slot_at = [&](int u) -> const char* { return smem + u * C::SLOT; };
 
   // S^T of the tile in ring slot u into a biased int32 accumulator: fragment loads and MFMAs
   // separately, so the K loads of tile t+1 can be issued ahead of the V-operand loads of tile t
-  // kf: the K fragments, then (C::QLDS) the Q fragments
   auto qk_load = [&](int u, v4i* kf) {
     const char* kl = slot_at(u);
 #pragma unroll
     for (int s = 0; s < C::NKS; ++s) kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s]);
-    if constexpr (C::QLDS != 0) {
-#pragma unroll
-      for (int s = 0; s < C::NKS; ++s) kf[C::NKS + s] = *reinterpret_cast<const v4i*>(q_lds + s * 1024);
-    }
   };
   auto qk_mma = [&](const v4i* kf) -> v16i {
-    const v4i* qv = C::QLDS != 0 ? kf + C::NKS : qf;
-    v16i acc = mfma_i8(kf[0], qv[0], C::QK_BIAS ? kmag : v16i{});
+    v16i acc = mfma_i8(kf[0], qf[0], C::QK_BIAS ? kmag : v16i{});
 #pragma unroll
-    for (int s = 1; s < C::NKS; ++s) acc = mfma_i8(kf[s], qv[s], acc);
+    for (int s = 1; s < C::NKS; ++s) acc = mfma_i8(kf[s], qf[s], acc);
     return acc;
   };
 
   // first half of the softmax of tile t: row max, d = f16(S - rm), deferred running max, er, and
   // the tile's P.V scale
-  //   mid: run after the running-max update (LATE_S: the first P.V half's dequantisation and the
-  //   second half's MFMAs), before the S conversion when LATE_S
-  auto sm1 = [&](const v16i& acc_in, int t, SmTile& st, float ckt, float svqt, auto&& mid) {
+  auto sm1 = [&](const v16i& acc_in, int t, SmTile& st, float ckt, float svqt) {
     // causal tiles crossing this wave's diagonal: keys above the row's query drop out of the max
     // (INT_MIN) and get d = -inf below, so P = 0 and the tile scale ignores them
     const bool diag = CAUSAL && (t * C::KT + C::KT - 1 > q0 + qoff);
@@ -271,35 +250,26 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     // S = f16(X * c) (int8:200-203: fp32 products, then fp16)
     v2h s2[8];
     _Float16 rm;
-    const float c = C::QK_BIAS ? kmag_scale(cq * ckt) : cq * ckt;
-    const float nb = -KMAG * c;
     if constexpr (C::QK_BIAS) {   // on the biased accumulator (QA_FWD_S_PK: packed f32, else fma_mix)
+      const float c = kmag_scale(cq * ckt);
+      const float nb = -KMAG * c;
 #if QA_FWD_S_PK
       rm = biased_to_f16(mx, c, nb);
+      biased_to_f16x16(acc, c, nb, s2);
 #else
       rm = fma_mix1(__int_as_float(mx), c, nb);
+      fma_mix16_after(acc, c, nb, mx, s2);
 #endif
     } else {
+      const float c = cq * ckt;
       rm = (_Float16)((float)mx * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        s2[j] = __builtin_bit_cast(v2h, pk_f16((float)acc[2 * j] * c, (float)acc[2 * j + 1] * c));
     }
-    // S = f16(X c) and d = f16(S - rm)  (int8:211, 232-236)
-    auto s_and_d = [&]() {
-      if constexpr (C::QK_BIAS) {
-#if QA_FWD_S_PK
-        biased_to_f16x16(acc, c, nb, s2);
-#else
-        fma_mix16_after(acc, c, nb, mx, s2);
-#endif
-      } else {
+    const v2h rm2 = {rm, rm};
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          s2[j] = __builtin_bit_cast(v2h, pk_f16((float)acc[2 * j] * c, (float)acc[2 * j + 1] * c));
-      }
-      const v2h rm2 = {rm, rm};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;
-    };
-    if constexpr (!LATE_S) s_and_d();
+    for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;   // f16(S - rm)  (int8:211, 232-236)
     if constexpr (CAUSAL || QA_FWD_LITERAL_P) {
       // Diagonal tiles keep few keys per row, where one P_i8 step weighs much in O: there P_i8
       // follows the reference chain literally (int8:205-237): next_m = max(m, rm) with the
@@ -349,8 +319,6 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     st.er = exp2_f32((float)(_Float16)(rm - m));
     if constexpr (PV != PV_I8) st.cpv = (float)(_Float16)(st.er * (1.0f / 127.0f));
     else st.cpv = st.er * svqt;
-    mid();
-    if constexpr (LATE_S) s_and_d();
   };
 
   // second half: e = exp2(d) (sm2_exp), then l += er * sum e and the P operand (sm2)
@@ -416,10 +384,8 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       for (int b = 0; b < C::NDB; ++b) va[b] = *reinterpret_cast<const v4i*>(vl + voff[b]);
     }
   };
-  // PV_I8: int32 products of d blocks [b0, b1) (pacc[b % NPACC])
-  constexpr int NPACC = PV != PV_I8 ? 1 : LATE_S ? C::NDB / 2 : C::NDB;
-  v16i pacc[NPACC];
-  auto pv_mma = [&](const VFrag* va, const v4u* pw, int b0 = 0, int b1 = C::NDB) {
+  v16i pacc[PV == PV_I8 ? C::NDB : 1];
+  auto pv_mma = [&](const VFrag* va, const v4u* pw) {
     if constexpr (PV != PV_I8) {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -429,24 +395,24 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     } else {
       const v4i p = __builtin_bit_cast(v4i, pw[0]);
 #pragma unroll
-      for (int b = b0; b < b1; ++b) pacc[b % NPACC] = mfma_i8(va[b], p, kmag);
+      for (int b = 0; b < C::NDB; ++b) pacc[b] = mfma_i8(va[b], p, kmag);
     }
   };
-  // PV_I8: O += (KMAG + X) * (sp * sv) for the tile's exact int32 X (one fused op per element), d
-  // blocks [b0, b1); the caller adds cpv to obias once per tile
-  auto pv_dequant = [&](float cpv, int b0 = 0, int b1 = C::NDB) {
+  // PV_I8: O += (KMAG + X) * (sp * sv) for the tile's exact int32 X (one fused op per element)
+  auto pv_dequant = [&](float cpv) {
     if constexpr (PV == PV_I8) {
       // explicit v_pk_fma_f32 pairs (scalar v_fma_f32 measured 2-3 % slower)
       const v2f_ c2 = {cpv, cpv};
 #pragma unroll
-      for (int b = b0; b < b1; ++b)
+      for (int b = 0; b < C::NDB; ++b)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const v2f_ a = {__int_as_float(pacc[b % NPACC][r]), __int_as_float(pacc[b % NPACC][r + 1])};
+          const v2f_ a = {__int_as_float(pacc[b][r]), __int_as_float(pacc[b][r + 1])};
           const v2f_ y = __builtin_elementwise_fma(a, c2, v2f_{o[b][r], o[b][r + 1]});
           o[b][r] = y[0];
           o[b][r + 1] = y[1];
         }
+      obias += cpv;
     }
   };
 
@@ -467,7 +433,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     // SM1(t+1) and the wave stalls on it): fragment reads, the 16 exponentials of tile t (which
     // cover the LDS latency), QK(t+1), then the rest of SM2(t), PV(t) and SM1(t+1).
     const int tn = min(t + 1, nt - 1);
-    v4i kf[C::QLDS != 0 ? 2 * C::NKS : C::NKS];
+    v4i kf[C::NKS];
     qk_load(nxt, kf);
     VFrag va[NVF];
     pv_load(cur, va);
@@ -479,32 +445,22 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     v4u pw[2];
     sm2(st, e, pw);
     cpv_pend = st.cpv;
-    if constexpr (LATE_S) {
-      pv_mma(va, pw, 0, 2);
-      sm1(nacc, tn, st, ckn, svqn, [&] {   // (may rescale O, obias and cpv_pend)
-        pv_dequant(cpv_pend, 0, 2);
-        pv_mma(va, pw, 2, 4);
-      });
-      pv_dequant(cpv_pend, 2, 4);
-    } else {
-      pv_mma(va, pw);
-      sm1(nacc, tn, st, ckn, svqn, [] {});   // (may rescale O, obias and cpv_pend)
-      pv_dequant(cpv_pend);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
-    }
-    if constexpr (PV == PV_I8) obias += cpv_pend;
+    pv_mma(va, pw);
+    sm1(nacc, tn, st, ckn, svqn);   // (may rescale O, obias and cpv_pend)
+    pv_dequant(cpv_pend);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
   };
   if (active) {
     {
-      v4i kf[C::QLDS != 0 ? 2 * C::NKS : C::NKS];
+      v4i kf[C::NKS];
       qk_load(0, kf);
-      sm1(qk_mma(kf), 0, st, ck0, svq0, [] {});
+      sm1(qk_mma(kf), 0, st, ck0, svq0);
     }
     // groups of NSLOT = 4 tiles with compile-time ring slots (immediate LDS offsets, one 16-B read
     // of each scale table per group), then the remaining tiles with run-time slots.  Only where the
     // unrolled body fits the register budget: the causal kernel (diagonal-tile masks and the literal
     // P chain) and the 3-wave f16 P.V kernel spill with it, so they keep the run-time-slot loop.
     static_assert(C::NSLOT == 4, "ring of 4 slots");
-    constexpr bool UNROLL = PV == PV_I8 && !CAUSAL && QA_FWD_OCC_I8 == 2;
+    constexpr bool UNROLL = PV == PV_I8 && !CAUSAL;
     int t = 0;
     for (; UNROLL && t + 4 <= nt; t += 4) {
       const v4f ck4 = *reinterpret_cast<const v4f*>(ck_lds + t);
@@ -555,7 +511,7 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
                       long sk_tok, int group, int qoff, float qks, hipStream_t st) {
   using C = Int8FwdCfg<D, PV>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
-  const int lds = C::TAB + (int)((((sk_tok / 32) + 3) / 4 * 4) * 4 * (PV == PV_I8 ? 2 : 1));
+  const int lds = C::RING + (int)((((sk_tok / 32) + 3) / 4 * 4) * 4 * (PV == PV_I8 ? 2 : 1));
   { static int granted_ = 0; lds_grant((const void*)int8_attn_fwd_kernel<D, PV, CAUSAL>, lds, granted_); }
   hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV, CAUSAL>), dim3((unsigned)(nq * bh)),
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
@@ -604,7 +560,7 @@ static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, 
   using C = Int8FwdCfg<D, PV_I8>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int nsplit = (int)((sk_tok + ks - 1) / ks);
-  const int lds = C::TAB + (int)((((ks / 32) + 3) / 4 * 4) * 8);
+  const int lds = C::RING + (int)((((ks / 32) + 3) / 4 * 4) * 8);
   { static int granted_ = 0; lds_grant((const void*)int8_attn_fwd_kernel<D, PV_I8, false, true>, lds, granted_); }
   hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV_I8, false, true>), dim3((unsigned)(nq * bh), (unsigned)nsplit),
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,

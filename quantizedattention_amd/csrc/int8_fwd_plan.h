@@ -20,9 +20,6 @@ enum PvMode { PV_F16 = 0, PV_I8 = 1 };
 #ifndef QA_FWD_OCC_F16
 #define QA_FWD_OCC_F16 3
 #endif
-#ifndef QA_FWD_OCC_I8
-#define QA_FWD_OCC_I8 2
-#endif
 #ifndef QA_FWD_QK_BIAS
 #define QA_FWD_QK_BIAS -1
 #endif
@@ -64,16 +61,12 @@ struct Int8FwdCfg {
   static constexpr int IPW = (INST + WAVES - 1) / WAVES;   // per wave, padded (counted vmcnt)
   // waves per SIMD the register budget must allow (__launch_bounds__ second argument): two (<= 256
   // VGPRs), three for the PV_F16 kernel at QA_FWD_OCC_F16 = 3 with 4-wave workgroups
-  static constexpr int WPS = (PV == PV_F16 && WAVES == 4) ? QA_FWD_OCC_F16 : QA_FWD_OCC_I8;
+  static constexpr int WPS = (PV == PV_F16 && WAVES == 4) ? QA_FWD_OCC_F16 : 2;
   static constexpr bool QK_BIAS = QA_FWD_QK_BIAS < 0 ? PV == PV_I8 : QA_FWD_QK_BIAS != 0;
   // the ring, reused as the output staging area of the epilogue
   static constexpr int STAGE = WAVES * RowTile<D, _Float16>::BYTES;
   static constexpr int RING = NSLOT * SLOT > STAGE ? NSLOT * SLOT : STAGE;
   static constexpr float THR = QA_FWD_THR;   // deferred running-max threshold (log2 units)
-  // 3-wave PV_I8 kernel: each wave's Q fragments in LDS (NKS 1-KiB pieces per wave) instead of 16
-  // registers; then the per-tile scale tables
-  static constexpr int QLDS = (PV == PV_I8 && WPS == 3 && D == 128) ? WAVES * NKS * 1024 : 0;
-  static constexpr int TAB = RING + QLDS;
 };
 
 template <int D>
