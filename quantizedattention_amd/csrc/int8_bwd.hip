@@ -207,12 +207,6 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #ifndef QA_DKV_NSLOT
 #define QA_DKV_NSLOT 4
 #endif
-// Packed fp32 (v_pk_*_f32, A/B bit mask): 1 = the S / dP arguments of one score in one v_pk_fma_f32
-// ({S, dP} * {c1, c2} - {lse, D}), 2 = the P quantiser's two fma steps on pairs, 4 = the dS
-// quantiser's two multiplies on pairs.  Same IEEE operations per element: bit-identical.
-#ifndef QA_BWD_PK
-#define QA_BWD_PK 0
-#endif
 // cache policy of the dS record stores (builtin aux: 2 = nt, 16 = sc1)
 #ifndef QA_BWD_PACK_ASM
 #define QA_BWD_PACK_ASM 1
@@ -325,23 +319,6 @@ QA_DEVICE void floor_magic16(float* y, float inv) {
         "+v"(y[7]), "+v"(y[8]), "+v"(y[9]), "+v"(y[10]), "+v"(y[11]), "+v"(y[12]), "+v"(y[13]),
         "+v"(y[14]), "+v"(y[15])
       : "v"(inv), "s"(magic));
-}
-
-// floor_magic16 on 8 pairs (v_pk_fma_f32): the same per-element operation
-QA_DEVICE void floor_magic16_pk(v2f_* y, float inv) {
-  const v2f_ iv = {inv, inv};
-  const v2f_ mg = {8388608.0f, 8388608.0f};
-  asm("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 2), 3\n\t"
-      "s_nop 1\n\t"
-      "v_pk_fma_f32 %0, %0, %8, %9\n\tv_pk_fma_f32 %1, %1, %8, %9\n\t"
-      "v_pk_fma_f32 %2, %2, %8, %9\n\tv_pk_fma_f32 %3, %3, %8, %9\n\t"
-      "v_pk_fma_f32 %4, %4, %8, %9\n\tv_pk_fma_f32 %5, %5, %8, %9\n\t"
-      "v_pk_fma_f32 %6, %6, %8, %9\n\tv_pk_fma_f32 %7, %7, %8, %9\n\t"
-      "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 2), 0\n\t"
-      "s_nop 1"
-      : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]),
-        "+v"(y[7])
-      : "v"(iv), "v"(mg));
 }
 
 // The int8 bytes of 16 integer-valued floats in [-127, 127], packed low to high (byte j of the
@@ -541,22 +518,10 @@ void int8_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
-          if constexpr ((QA_BWD_PK & 1) && G::WANT_DS) {
-            // {S c1 - lse, dP c2 - D} in one packed fma: {lse, D} of the row are adjacent in LDS
-            const v2f_ ld2 = j == 0 ? v2f_{a[0], a[1]} : j == 1 ? v2f_{a[2], a[3]}
-                           : j == 2 ? v2f_{b[0], b[1]} : v2f_{b[2], b[3]};
-            const v2f_ y = __builtin_elementwise_fma(v2f_{(float)sa[i], (float)pa[i]},
-                                                     v2f_{c1, c2}, -ld2);
-            float p = exp2_f32(y[0]);
-            if (MASK && dd > 8 * g + j) p = 0.f;
-            if constexpr (G::WANT_P) P[i] = p;
-            dS[i] = p * y[1];
-          } else {
           float p = exp2_f32(fmaf((float)sa[i], c1, -lse_r[j]));
           if (MASK && dd > 8 * g + j) p = 0.f;   // key > query: x0 + c32 > y0 + 8g + 4h + j
           if constexpr (G::WANT_P) P[i] = p;
           if constexpr (G::WANT_DS) dS[i] = p * fmaf((float)pa[i], c2, -d_r[j]);
-          }
         }
       }
     } else {
@@ -590,26 +555,7 @@ void int8_bwd_kernel(
     const float c = sx * so;
     const float nc = -8388608.0f * c;
     float y[16];
-#if QA_BWD_PK & 2
-    {
-      v2f_ y2[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) y2[k] = v2f_{X[2 * k], X[2 * k + 1]};
-      floor_magic16_pk(y2, inv);
-      const v2f_ c2v = {c, c}, nc2 = {nc, nc};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        v4u w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const v2f_ z = __builtin_elementwise_fma(y2[4 * s + j], c2v, nc2);
-          w[j] = pk_bf16(z[0], z[1]);
-        }
-        op[s] = __builtin_bit_cast(v8bf, w);
-      }
-      return;
-    }
-#elif QA_BWD_PACK_ASM
+#if QA_BWD_PACK_ASM
 #pragma unroll
     for (int i = 0; i < 16; ++i) y[i] = X[i];
     floor_magic16(y, inv);
@@ -684,27 +630,6 @@ void int8_bwd_kernel(
       const float inv = xmax > 0.f ? 127.0f * __builtin_amdgcn_rcpf(xmax) : 0.f;
       const float c = sx * so_ds(t);
       float q[16];
-#if QA_BWD_PK & 4
-      {
-        const v2f_ iv = {inv, inv}, c2v = {c, c};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const v2f_ z = v2f_{X[2 * k], X[2 * k + 1]} * iv;
-          q[2 * k] = __builtin_truncf(z[0]);
-          q[2 * k + 1] = __builtin_truncf(z[1]);
-        }
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          v4u w;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const v2f_ z = v2f_{q[8 * s + 2 * j], q[8 * s + 2 * j + 1]} * c2v;
-            w[j] = pk_bf16(z[0], z[1]);
-          }
-          op[s] = __builtin_bit_cast(v8bf, w);
-        }
-      }
-#else
 #pragma unroll
       for (int i = 0; i < 16; ++i) q[i] = __builtin_truncf(X[i] * inv);
 #pragma unroll
@@ -714,7 +639,6 @@ void int8_bwd_kernel(
         for (int j = 0; j < 4; ++j) w[j] = pk_bf16(q[8 * s + 2 * j] * c, q[8 * s + 2 * j + 1] * c);
         op[s] = __builtin_bit_cast(v8bf, w);
       }
-#endif
 #if QA_BWD_PACK_ASM
       const v4i bytes = pack16_i8(q);
 #else

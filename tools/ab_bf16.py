@@ -2,6 +2,7 @@
 
     python tools/ab_bf16.py [B,H,S,D] [causal] [f = forward only]
 """
+import hashlib
 import math
 import os
 import sys
@@ -43,6 +44,8 @@ fwd_only = len(sys.argv) > 3 and sys.argv[3] == "f"
 tb = 1.0 if fwd_only else timed(lambda: helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, causal, dO))
 flop = 4 * B * H * S * S * D
 peak = 256 * 4096 * 2.4e9
-print(f"{os.environ.get('QATTN_LIB', 'default')}: fwd {tf * 1e3:.1f} us "
+O, lse = helion_atten_bf16_fwd_training(q, k, v, causal)
+digest = hashlib.sha256(O.cpu().numpy().tobytes() + lse.cpu().numpy().tobytes()).hexdigest()[:12]
+print(f"{os.environ.get('QATTN_LIB', 'default')}: O/lse {digest}  fwd {tf * 1e3:.1f} us "
       f"({flop / tf / 1e9:.0f} TFLOP/s, {flop / tf / 1e-3 / peak * 100:.1f}% bf16 peak)  "
       f"bwd {tb * 1e3:.1f} us ({2.5 * flop / tb / 1e9:.0f} TFLOP/s)", flush=True)
