@@ -89,6 +89,10 @@ constexpr int fwd_wps() { return CAUSAL ? 2 : Int8FwdCfg<D, PV>::WPS; }
 #define QA_FWD_STAMP 0
 #endif
 
+// QA_FWD_UNROLL (A/B): 0 keeps the run-time-slot loop for every instantiation
+#ifndef QA_FWD_UNROLL
+#define QA_FWD_UNROLL 1
+#endif
 #if QA_FWD_STAMP
 __device__ unsigned long long g_fwd_stamp[8192][4];
 #define FWD_STAMP(k)                                                                            \
@@ -460,7 +464,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     // unrolled body fits the register budget: the causal kernel (diagonal-tile masks and the literal
     // P chain) and the 3-wave f16 P.V kernel spill with it, so they keep the run-time-slot loop.
     static_assert(C::NSLOT == 4, "ring of 4 slots");
-    constexpr bool UNROLL = PV == PV_I8 && !CAUSAL;
+    constexpr bool UNROLL = PV == PV_I8 && !CAUSAL && QA_FWD_UNROLL;
     int t = 0;
     for (; UNROLL && t + 4 <= nt; t += 4) {
       const v4f ck4 = *reinterpret_cast<const v4f*>(ck_lds + t);

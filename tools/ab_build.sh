@@ -9,8 +9,10 @@ python3 -c "import sys; sys.path.insert(0, '$R'); from quantizedattention_amd im
 mkdir -p $R/_ab/obj
 OBJ=$R/_ab/obj/$(basename $SRC .hip)_$NAME.o
 case $SRC in /*) SRCP=$SRC ;; *) SRCP=$R/quantizedattention_amd/csrc/$SRC ;; esac
+# the product build's per-source flags (build.FILE_FLAGS), so a variant differs only by "$@"
+FF=$(python3 -c "import sys; sys.path.insert(0, '$R'); from quantizedattention_amd import build; print(' '.join(build.FILE_FLAGS.get('$(basename $SRC)', [])))")
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt \
-  -fno-gpu-rdc -Wno-unused-result -Wno-unused-value -I$R/include -I$R/quantizedattention_amd/csrc "$@" -c $SRCP -o $OBJ
+  -fno-gpu-rdc -Wno-unused-result -Wno-unused-value -I$R/include -I$R/quantizedattention_amd/csrc $FF "$@" -c $SRCP -o $OBJ
 OTHERS=$(ls $R/quantizedattention_amd/_build/*.o | grep -v "/dev_" | grep -v "/$(basename $SRC .hip).o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/_ab/libqattn_$NAME.so $OTHERS $OBJ
 echo "built _ab/libqattn_$NAME.so"
