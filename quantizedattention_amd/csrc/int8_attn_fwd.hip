@@ -224,10 +224,12 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
 
   // first half of the softmax of tile t: row max, d = f16(S - rm), deferred running max, er, and
   // the tile's P.V scale
-  auto sm1 = [&](const v16i& acc_in, int t, SmTile& st, float ckt, float svqt) {
+  //   dg (std::true_type / false_type): whether tile t may cross the diagonal (causal), i.e.
+  //   whether the masks and the literal P chain are compiled in
+  auto sm1 = [&](const v16i& acc_in, int t, SmTile& st, float ckt, float svqt, auto dg) {
     // causal tiles crossing this wave's diagonal: keys above the row's query drop out of the max
     // (INT_MIN) and get d = -inf below, so P = 0 and the tile scale ignores them
-    const bool diag = CAUSAL && (t * C::KT + C::KT - 1 > q0 + qoff);
+    const bool diag = CAUSAL && decltype(dg)::value && (t * C::KT + C::KT - 1 > q0 + qoff);
     // QA_FWD_LITERAL_P: the reference's literal P_i8 chain on every tile (priced)
     const bool lit = diag || (QA_FWD_LITERAL_P != 0);
     v16i acc = acc_in;
@@ -430,7 +432,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   // (its row max cannot move m) and it keeps the loop body branch-free.
   //   cur, nxt: ring slots of tiles t and t+1; fill: the slot the DMA of tile t+3 goes to (freed by
   //   the barrier); ckn, svqn: the scales of tile t+1
-  auto iter = [&](int t, int cur, int nxt, int fill, float ckn, float svqn) {
+  auto iter = [&](int t, int cur, int nxt, int fill, float ckn, float svqn, auto dg) {
     ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot `fill` is free
     dma.issue(smem_lds + fill * C::SLOT, min(t + 3, nt - 1));
     // Phase order (pinned: hipcc otherwise issues the QK(t+1) chain right before its consumer
@@ -450,32 +452,42 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     sm2(st, e, pw);
     cpv_pend = st.cpv;
     pv_mma(va, pw);
-    sm1(nacc, tn, st, ckn, svqn);   // (may rescale O, obias and cpv_pend)
+    sm1(nacc, tn, st, ckn, svqn, dg);   // (may rescale O, obias and cpv_pend)
     pv_dequant(cpv_pend);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
   };
   if (active) {
     {
       v4i kf[C::NKS];
       qk_load(0, kf);
-      sm1(qk_mma(kf), 0, st, ck0, svq0);
+      sm1(qk_mma(kf), 0, st, ck0, svq0, std::true_type{});
     }
+    // Causal: iteration t runs SM1 of tile t+1, and tiles below td0 = (first query of the workgroup
+    // + qoff) / KT cross no wave's diagonal, so iterations t < td0 - 1 run with the masks and the
+    // literal P chain compiled out (the same values: nothing is masked there) and the rest, at
+    // most WAVES + 1 of them, with them.
+    const int tmain = CAUSAL ? max(0, min(nt, (qt * C::QROWS + qoff) / C::KT - 1)) : nt;
     // groups of NSLOT = 4 tiles with compile-time ring slots (immediate LDS offsets, one 16-B read
     // of each scale table per group), then the remaining tiles with run-time slots.  Only where the
-    // unrolled body fits the register budget: the causal kernel (diagonal-tile masks and the literal
-    // P chain) and the 3-wave f16 P.V kernel spill with it, so they keep the run-time-slot loop.
+    // unrolled body fits the register budget (the 3-wave f16 P.V kernel spills with it).
     static_assert(C::NSLOT == 4, "ring of 4 slots");
-    constexpr bool UNROLL = PV == PV_I8 && !CAUSAL && QA_FWD_UNROLL;
+    constexpr bool UNROLL = PV == PV_I8 && QA_FWD_UNROLL;
+    const std::false_type nodiag{};
     int t = 0;
-    for (; UNROLL && t + 4 <= nt; t += 4) {
+    for (; UNROLL && t + 4 <= tmain; t += 4) {
       const v4f ck4 = *reinterpret_cast<const v4f*>(ck_lds + t);
       const v4f sv4 = PV == PV_I8 ? *reinterpret_cast<const v4f*>(svq_lds + t) : v4f{};
-      iter(t, 0, 1, 3, ck4[0], sv4[0]);
-      iter(t + 1, 1, 2, 0, ck4[1], sv4[1]);
-      iter(t + 2, 2, 3, 1, ck4[2], sv4[2]);
-      iter(t + 3, 3, 0, 2, ck4[3], sv4[3]);
+      iter(t, 0, 1, 3, ck4[0], sv4[0], nodiag);
+      iter(t + 1, 1, 2, 0, ck4[1], sv4[1], nodiag);
+      iter(t + 2, 2, 3, 1, ck4[2], sv4[2], nodiag);
+      iter(t + 3, 3, 0, 2, ck4[3], sv4[3], nodiag);
     }
-    for (; t < nt; ++t)
-      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], PV == PV_I8 ? svq_lds[t] : 0.f);
+    for (; t < tmain; ++t)
+      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], PV == PV_I8 ? svq_lds[t] : 0.f, nodiag);
+    if constexpr (CAUSAL) {
+      for (; t < nt; ++t)
+        iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], PV == PV_I8 ? svq_lds[t] : 0.f,
+             std::true_type{});
+    }
   } else {   // a wave past the last query row: the barriers and the ring's DMA only
     for (int t = 0; t < nt; ++t) {
       ring_wait_barrier<C::IPW>();
