@@ -4,6 +4,9 @@ describes how it was built).  Run through tools/ab_run.sh; equal hashes across v
 
     python tools/ab_pair.py            (env CHUNKS="0,32,64": key/value heads per chunk, 0 = one pass)"""
 import hashlib, os, sys, torch
+# the package loads QATTN_LIB: point it at the variant tools/ab_run.sh names in QATTN_AB
+if os.environ.get("QATTN_AB"):
+    os.environ["QATTN_LIB"] = os.environ["QATTN_AB"]
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward
 
