@@ -126,7 +126,6 @@ def int8_kernel_times(q, k, v, dO, n):
     e = lambda *shape, dt: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
     qi, ki, vi, dOi = (e(N, D, dt=torch.int8) for _ in range(4))
     sq, sk, sv, sdO = (e(N // 32, dt=torch.float16) for _ in range(4))
-    vdq = e(N, D, dt=torch.float16)
     vt = e(N, D, dt=torch.int8)
     km = e(B * H, D, dt=torch.float16)
     O = e(B, H, S, D, dt=torch.float16)
@@ -143,17 +142,18 @@ def int8_kernel_times(q, k, v, dO, n):
                                                      P(kb), P(km), N, S, D, st),
         "quant_block32_kernel(q)": lambda: _lib.call("qattn_int8_quant_img", P(q), P(qi), P(sq), None,
                                                      P(qb), None, N, S, D, st),
-        "quant_block32_kernel(v)": lambda: _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq),
-                                                     None, N, S, D, st),
+        "quant_kv_kernel": lambda: _lib.call("qattn_int8_quant_kv", P(k), P(ki), P(sk), P(kb), P(km), P(v),
+                                             P(vi), P(sv), P(vt), N, S, D, st),
         "quant_vt_kernel(v)": lambda: _lib.call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D,
                                                 st),
         # the default forward: P.V on the int8 MFMA (the reference's hl.dot(P_i8, v_i8))
-        "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki),
+        "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki),
                                                   P(sk), P(vt), P(sv), P(O), P(lse), B * H, S, S, 1, 0,
                                                   D, qks, st),
-        "int8_attn_fwd_kernel<f16 P.V>": lambda: _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki),
-                                                           P(sk), P(vdq), P(O), P(lse), B * H, S, D,
-                                                           qks, st),
+        # the forward the drop-ins run: q quantised inside the attention kernel
+        "int8_attn_fwd_kernel<q fused>": lambda: _lib.call("qattn_int8_attn_fwd_qf", P(q), P(qi), P(sq), P(qb),
+                                                           P(ki), P(sk), P(vt), P(sv), P(O), P(lse), B * H,
+                                                           S, S, 1, 0, D, qks, st),
         "int8_bwd_prep": lambda: _lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(lse), P(dOi), P(sdO),
                                            P(LD), P(ob), B * H, S, D, st),
         "int8_bwd_dkdv_kernel<dK+dV>": lambda: _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi),

@@ -59,6 +59,12 @@ int qattn_int8_dequant(const void* idx, const void* scale, void* deq, long rows,
  *   v_mfma_i32_32x32x32_i8 in the forward's key order).  rows % 32 == 0. */
 int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt, long rows, int head_dim,
                         void* stream);
+/* k and v of one forward in one launch: qattn_int8_quant_img on k (kmean / k_img optional, as
+ * there) and qattn_int8_quant_vt on v, both [rows, D] with rows_per_head rows per head; the same
+ * outputs bit for bit. */
+int qattn_int8_quant_kv(const void* k, void* k_i8, void* sk, void* k_img, const void* kmean,
+                        const void* v, void* v_i8, void* sv, void* vt, long rows, int rows_per_head,
+                        int head_dim, void* stream);
 /* vt of qattn_int8_quant_vt from stored indices v_i8 (a restored int8 key/value cache). */
 int qattn_int8_v_image(const void* v_i8, void* vt, long rows, int head_dim, void* stream);
 
@@ -67,12 +73,15 @@ int qattn_int8_v_image(const void* v_i8, void* vt, long rows, int head_dim, void
 int qattn_kmean(const void* k, void* kmean, long bh, long seq, int head_dim, void* stream);
 
 /* int8 SageAttention-3 forward, per (batch, head) (attention_int8.py:197-257; per-head contract F2).
- *   q_i8, k_i8  i8 [bh*seq, D]; sq, sk f16 [bh*seq/32]; vdq f16 [bh*seq, D] (= qattn_int8_quant deq
- *   of v); out O f16 [bh*seq, D]; lse f16 [bh*seq] (base 2).  S = f16(f32(q_i8.k_i8) * sq*sk*qks),
- *   P = exp2(S - m), P.V on int8-quantised P (sp = exp2(rowmax - m)/127).  seq % 32 == 0. */
+ *   q_i8, k_i8  i8 [bh*seq, D]; sq, sk, sv f16 [bh*seq/32]; vt = the V^T operand image of
+ *   qattn_int8_quant_vt; out O f16 [bh*seq, D]; lse f16 [bh*seq] (base 2).
+ *   S = f16(f32(q_i8.k_i8) * sq*sk*qks), P = exp2(S - m), P_i8 = trunc(P / sp) with sp =
+ *   exp2(rowmax - m)/127, and the P.V contraction on the int8 MFMA as the reference's
+ *   hl.dot(P_int8, v_int8) (int8:249): each 32-key tile's exact int32 product is dequantised by
+ *   sp * sv (int8:249-250).  seq % 32 == 0. */
 int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                        const void* vdq, void* out, void* lse, long bh, long seq, int head_dim,
-                        float qks, void* stream);
+                        const void* vt, const void* sv, void* out, void* lse, long bh, long seq,
+                        int head_dim, float qks, void* stream);
 
 /* Generalised shapes (the reference's int8 path has none of these): bh = batch *
  * query heads with sq_tok query rows each; the key/value tensors have bh / group heads of sk_tok
@@ -83,19 +92,20 @@ int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, cons
  * query rows and the key/value rows separately.  sq_tok % 32 == sk_tok % 32 == 0, bh % group == 0.
  * qattn_int8_attn_fwd is this with sq_tok = sk_tok = seq, group = 1, causal = 0. */
 int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                           const void* vdq, void* out, void* lse, long bh, long sq_tok, long sk_tok,
-                           int group, int causal, int head_dim, float qks, void* stream);
+                           const void* vt, const void* sv, void* out, void* lse, long bh,
+                           long sq_tok, long sk_tok, int group, int causal, int head_dim,
+                           float qks, void* stream);
 
-/* qattn_int8_attn_fwd_ex with the P.V contraction on the int8 MFMA, as the reference's
- * hl.dot(P_int8, v_int8) (attention_int8.py:249): vt = the V^T image of qattn_int8_quant_vt, sv its
- * block scales; each 32-key tile's exact int32 product is dequantised by sp * sv (int8:249-250).
- * Same outputs and conventions as qattn_int8_attn_fwd_ex. */
-int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                                const void* vt, const void* sv, void* out, void* lse, long bh,
-                                long sq_tok, long sk_tok, int group, int causal, int head_dim,
-                                float qks, void* stream);
+/* qattn_int8_attn_fwd_ex quantising q inside the attention kernel (the reference quantises inside its
+ * forward, attention_int8.py:178-186): q f16 [bh*sq_tok, D] in; q_i8 i8 [bh*sq_tok, D] and sq f16
+ * [bh*sq_tok/32] out, bit-exact with qattn_int8_quant; q_bf bf16 [bh*sq_tok, D] = bf16(q_i8) out
+ * (the backward's image) when not NULL.  O and lse as qattn_int8_attn_fwd_ex on those q_i8, sq. */
+int qattn_int8_attn_fwd_qf(const void* q, void* q_i8, void* sq, void* q_bf, const void* k_i8,
+                           const void* sk, const void* vt, const void* sv, void* out, void* lse,
+                           long bh, long sq_tok, long sk_tok, int group, int causal, int head_dim,
+                           float qks, void* stream);
 
-/* Key-split (flash-decoding) form of qattn_int8_attn_fwd_i8pv_ex, non-causal, for short query blocks
+/* Key-split (flash-decoding) form of qattn_int8_attn_fwd_ex, non-causal, for short query blocks
  * against long key ranges (the int8 key/value cache): each workgroup covers
  * keys_per_split keys (multiple of 32) of its query rows and writes the partial softmax state
  *   opart f16 [nsplit][bh*sq_tok][D] = O_s / l_s (the key range's normalised output) and

@@ -40,6 +40,10 @@ int qattn_probe_quant_div(int s_lo, int s_hi, void* bad, void* stream);
  * (grid-stride): an RCCL-like few-workgroup copy for the overlap probe (tools/overlap_probe.py). */
 int qattn_probe_few_wg_copy(const void* src, void* dst, long bytes, int workgroups, void* stream);
 
+/* exp2 on every fp16 argument h (65536 bit patterns): e32[h] = bits of v_exp_f32((float)h) (uint32),
+ * e16[h] = bits of v_exp_f16(h) (uint16) -- tools/exp2_probe.py, tests/test_gpu_layout.py. */
+int qattn_probe_exp2_dom(void* e32, void* e16, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

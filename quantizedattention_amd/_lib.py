@@ -26,12 +26,13 @@ SIGNATURES = {
     "qattn_int8_quant_img": [_vp] * 6 + [_c_long, _c_int, _c_int, _vp],
     "qattn_int8_dequant": [_vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_int8_quant_vt": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
+    "qattn_int8_quant_kv": [_vp] * 9 + [_c_long, _c_int, _c_int, _vp],
     "qattn_int8_v_image": [_vp, _vp, _c_long, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
-    "qattn_int8_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_int, _c_float, _vp],
-    "qattn_int8_attn_fwd_ex": [_vp] * 7 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
-    "qattn_int8_attn_fwd_i8pv_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
+    "qattn_int8_attn_fwd": [_vp] * 8 + [_c_long, _c_long, _c_int, _c_float, _vp],
+    "qattn_int8_attn_fwd_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                  _vp],
+    "qattn_int8_attn_fwd_qf": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_split": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                _vp],
     "qattn_int8_split_combine": [_vp] * 4 + [_c_long, _c_int, _c_int, _vp],
@@ -89,6 +90,7 @@ DEV_SIGNATURES = {
     "qattn_probe_fwd_helpers": [_vp] * 7,
     "qattn_probe_quant_div": [_c_int, _c_int, _vp, _vp],
     "qattn_probe_few_wg_copy": [_vp, _vp, _c_long, _c_int, _vp],
+    "qattn_probe_exp2_dom": [_vp, _vp, _vp],
 }
 
 # return types other than the int status code
@@ -213,3 +215,32 @@ def require_gpu(*tensors: torch.Tensor) -> None:
         if not t.is_cuda:
             raise QAttnError("qattn kernels run on the GPU only; got a tensor on "
                              f"{t.device} (no CPU fallback by design)")
+
+
+# Backward workspaces (the dS records) refused by the allocator, per device: {device: smallest refused
+# size}.  torch's caching allocator answers an allocation it cannot serve by freeing every cached
+# block and retrying before it raises, so a training loop whose workspace never fits would flush the
+# cache and stall on hipFree in every backward.  After one refusal, a workspace that large is only
+# tried again when the device has room for it (free plus reserved-but-unused bytes).
+_WS_REFUSED: dict = {}
+
+
+def try_workspace(nbytes: int, device) -> torch.Tensor | None:
+    """A uint8 workspace of ``nbytes`` on ``device``, or None when it does not fit (the caller then
+    takes the recomputing path, with the same results)."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    refused = _WS_REFUSED.get(idx)
+    if refused is not None and nbytes >= refused:
+        free, _total = torch.cuda.mem_get_info(idx)
+        spare = torch.cuda.memory_reserved(idx) - torch.cuda.memory_allocated(idx)
+        if free + spare < nbytes:
+            return None
+    try:
+        ws = torch.empty((nbytes,), dtype=torch.uint8, device=dev)
+    except torch.cuda.OutOfMemoryError:
+        _WS_REFUSED[idx] = nbytes if refused is None else min(refused, nbytes)
+        return None
+    if refused is not None and nbytes >= refused:
+        _WS_REFUSED.pop(idx, None)
+    return ws

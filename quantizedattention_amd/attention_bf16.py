@@ -122,10 +122,9 @@ def helion_flash_atten_2_algo_4_bwd(
         ws_bytes = _lib.load().qattn_bf16_bwd_ws_bytes(B * H, S, Sk)
         cap = _lib.load().qattn_bwd_ws_cap() if WS_MAX_BYTES is None else WS_MAX_BYTES
         if 0 < ws_bytes <= cap:
-            try:
-                ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
-            except torch.cuda.OutOfMemoryError:
-                ws = None   # no room for the dS records: recompute dS in the dQ pass (same results)
+            # (None when there is no room for the dS records: recompute dS in the dQ pass, same
+            # results)
+            ws = _lib.try_workspace(ws_bytes, dev)
     if ws is not None:
         _lib.call("qattn_bf16_bwd_ws_ex", *args, _lib.ptr(ws), st)
     else:

@@ -59,27 +59,14 @@ def _check_shapes(q, k, v):
         raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
 
 
-# P.V contraction of the forward (csrc/int8_attn_fwd.hip):
-#   "i8": v_mfma_i32_32x32x32_i8 on P_i8 x v_i8, as the reference's hl.dot (int8:249), with one fused
-#         dequantisation per 32-key tile;
-#   "f16": v_mfma_f32_32x32x16_f16 on f16(P_i8 * sp) x f16(v_i8 * sv), the tile scale in the operands.
-# Same P_i8, scales and tolerance in both modes; QATTN_INT8_PV selects the default.  (The role-split
-# "rs" and two-tile "f2" forms of the f16 mode measured slower and were removed in round 4.)
-PV_MODES = ("i8", "f16")
-PV_MODE = os.environ.get("QATTN_INT8_PV", "i8")
-
-
-def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = False,
-                  pv: str | None = None):
-    """Quantise q, k, v and run the int8 attention forward.
+def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = False):
+    """Quantise q, k, v and run the int8 attention forward (csrc/int8_attn_fwd.hip: both
+    contractions on the int8 MFMA, P.V as the reference's hl.dot(P_int8, v_int8), int8:249).
 
     Returns (O, lse, q_i8, k_i8T, v_i8, sq, sk, sv, k_mean, q_bf, k_bf); q_bf / k_bf are the exact
     bf16 images of q_i8 / k_i8 the backward reads (written by the same quantiser pass when
-    ``images``, else None).  ``pv``: the P.V mode ("f16" / "i8", default PV_MODE).
+    ``images``, else None).
     """
-    pv = PV_MODE if pv is None else pv
-    if pv not in PV_MODES:
-        raise _lib.QAttnError(f"qattn int8: unknown P.V mode {pv!r} (one of {PV_MODES})")
     _check_shapes(q, k, v)
     _lib.require_gpu(q, k, v)
     q = q.to(torch.float16).contiguous()
@@ -97,8 +84,7 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     sq = torch.empty((N // BQ,), dtype=torch.float16, device=dev)
     sk = torch.empty((Nkv // BKV,), dtype=torch.float16, device=dev)
     sv = torch.empty((Nkv // BKV,), dtype=torch.float16, device=dev)
-    # P.V operand image of v: f16(v_i8 * sv) ("f16") or the int8 V^T operand image ("i8")
-    vop = torch.empty((Nkv, D), dtype=torch.int8 if pv == "i8" else torch.float16, device=dev)
+    vt = torch.empty((Nkv, D), dtype=torch.int8, device=dev)   # the int8 V^T operand image of v
     O = torch.empty((B, H, S, D), dtype=torch.float16, device=dev)
     lse = torch.empty((N,), dtype=torch.float16, device=dev)
     q_bf = k_bf = None
@@ -109,23 +95,15 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
     if smooth:
         k_mean = torch.empty((B, Hkv, 1, D), dtype=torch.float16, device=dev)
         _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(k_mean), B * Hkv, Sk, D, st)
-    _lib.call("qattn_int8_quant_img", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), None, _lib.ptr(q_bf),
-              None, N, S, D, st)
-    _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
-              _lib.ptr(k_mean), Nkv, Sk, D, st)
     qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
-    if pv == "f16":
-        _lib.call("qattn_int8_quant", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), None,
-                  Nkv, Sk, D, st)
-        _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8), _lib.ptr(sk),
-                  _lib.ptr(vop), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk, H // Hkv, int(bool(causal)),
-                  D, qks, st)
-    else:
-        _lib.call("qattn_int8_quant_vt", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vop), Nkv,
-                  D, st)
-        _lib.call("qattn_int8_attn_fwd_i8pv_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(k_i8),
-                  _lib.ptr(sk), _lib.ptr(vop), _lib.ptr(sv), _lib.ptr(O), _lib.ptr(lse), B * H, S, Sk,
-                  H // Hkv, int(bool(causal)), D, qks, st)
+    # k (smoothed, with the backward's bf16 image when asked) and v (with its P.V operand image) in
+    # one launch
+    _lib.call("qattn_int8_quant_kv", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), _lib.ptr(k_bf),
+              _lib.ptr(k_mean), _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vt), Nkv, Sk, D, st)
+    # q is quantised inside the attention kernel (q_i8, sq and the bf16 image written there)
+    _lib.call("qattn_int8_attn_fwd_qf", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(q_bf),
+              _lib.ptr(k_i8), _lib.ptr(sk), _lib.ptr(vt), _lib.ptr(sv), _lib.ptr(O), _lib.ptr(lse),
+              B * H, S, Sk, H // Hkv, int(bool(causal)), D, qks, st)
     # k_i8T is returned as the [D, N] view of the row-major [N, D] tensor (same values/shape as
     # int8:165, zero-copy).
     return O, lse, q_i8, k_i8.t(), v_i8, sq, sk, sv, k_mean, q_bf, k_bf
@@ -221,10 +199,8 @@ def _int8_backward(dO, q_i8, sq, k_i8T, sk, v_i8, sv, O, lse, q_bf=None, k_bf=No
                               "head; use the recomputing backward (use_ws=False)")
     ws = None
     if use_ws and ws_bytes > 0:
-        try:
-            ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
-        except torch.cuda.OutOfMemoryError:
-            ws = None   # no room for the workspace: recompute dS in the dQ pass (same results)
+        # (None when there is no room: recompute dS in the dQ pass, same results)
+        ws = _lib.try_workspace(ws_bytes, dev)
         if ws is not None and ws_poison is not None:
             ws.fill_(int(ws_poison) & 0xFF)
     if ws is not None and chunk < B * Hkv:

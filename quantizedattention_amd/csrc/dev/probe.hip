@@ -221,3 +221,22 @@ extern "C" int qattn_probe_few_wg_copy(const void* src, void* dst, long bytes, i
                      (const uint4*)src, (uint4*)dst, bytes / 16);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// exp2 on the fp16 domain: for every fp16 bit pattern h, e32[h] = v_exp_f32((float)h) and
+// e16[h] = v_exp_f16(h) (bits).  tools/exp2_probe.py compares them with the correctly rounded
+// values (the literal P chain of the int8 forward evaluates exp2 only at fp16 arguments).
+namespace qattn {
+__global__ __launch_bounds__(256) void probe_exp2_dom_kernel(unsigned* e32, unsigned short* e16) {
+  const unsigned i = blockIdx.x * 256 + threadIdx.x;
+  const _Float16 h = __builtin_bit_cast(_Float16, (unsigned short)i);
+  e32[i] = __float_as_uint(exp2_f32((float)h));
+  v2h x[4] = {{h, h}, {h, h}, {h, h}, {h, h}}, r[4];
+  exp2_pk4(x, r);
+  e16[i] = __builtin_bit_cast(unsigned short, r[0][1]);
+}
+}  // namespace qattn
+extern "C" int qattn_probe_exp2_dom(void* e32, void* e16, void* stream) {
+  hipLaunchKernelGGL(probe_exp2_dom_kernel, dim3(65536 / 256), dim3(256), 0, (hipStream_t)stream,
+                     (unsigned*)e32, (unsigned short*)e16);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

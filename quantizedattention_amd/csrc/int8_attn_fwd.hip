@@ -3,8 +3,7 @@
 //
 // Work decomposition
 //   * one workgroup = 4 waves = 128 query rows of one (b,h); wave w owns rows 32w..32w+31 = one
-//     32-token q-quant block (one sq scale per wave).  PV_I8: 2 workgroups per CU (<= 256 VGPRs);
-//     PV_F16: 3 (<= 168 VGPRs).
+//     32-token q-quant block (one sq scale per wave).  2 workgroups per CU (<= 256 VGPRs).
 //   * keys stream in 32-key tiles (= one Bkv block) through a 4-slot LDS ring filled by buffer
 //     LDS-DMA (no staging registers; the bank swizzle is applied to the per-lane source offset, the
 //     LDS image is written lane-linearly).  One barrier per tile; the DMA of tile t+3 is issued
@@ -14,14 +13,13 @@
 // Per 32-key tile and wave (swapped orientation: keys in registers, query on the lane pair l, l^32),
 // software-pipelined by one tile so that each wave has MFMA work beside its softmax VALU:
 //     QK(t+1)   S^T = K_i8 . Q_i8^T                   D/32 x v_mfma_i32_32x32x32_i8
-//     SM2(t)    e = exp2(d), l, P operand             (VALU, beside the QK(t+1) MFMAs)
-//     PV(t)     O^T += V^T . P^T                      (PV modes below)
+//     SM2(t)    e = exp2(d), l, P_i8                  (VALU, beside the QK(t+1) MFMAs)
+//     PV(t)     O^T += dequant(V^T . P_i8^T)          D/32 x v_mfma_i32_32x32x32_i8
 //     SM1(t+1)  d = S - rowmax, deferred running max  (VALU, beside the PV(t) MFMAs)
 // Reference rounding points (int8:197-257):
 //     S  = f16(acc * c),  c = sq*sk*qks          on the biased accumulator: one v_pk_fma_f32 per pair
-//                                                + v_cvt_pk_f16_f32 (QA_FWD_S_PK, default), or one
-//                                                v_fma_mix per score
-//                                                (common.h KMAG: no int -> float conversion)
+//                                                + v_cvt_pk_f16_f32 (common.h KMAG: no int -> float
+//                                                conversion)
 //     rm = f16(max_k(acc) * c)                   (c > 0: the row max commutes with the scaling)
 //     d  = f16(S - rm)                           (S rounded to f16 first, as the reference does)
 //     e  = exp2(d);  P_i8 = trunc(127 e);  sp = exp2(rm - m)/127  (int8:211-237)
@@ -30,21 +28,23 @@
 // exceeds it by more than THR = 8 (log2 units); P_i8 depends only on S - rowmax(tile), O and l share
 // the (possibly stale) reference, so O / l is unchanged up to rounding.
 //
-// P.V modes (int8:249-250, O += (P_i8 . v_i8) * sp * sv per 32-key tile):
-//   PV_F16            one v_mfma_f32_32x32x16_f16 chain on f16(P_i8 * sp) x f16(v_i8 * sv) (the
-//                     quantiser's vdq image): the tile scale rides in the operands, the fp32
-//                     accumulator needs no per-tile work.  P_i8 and the scales are the reference's;
-//                     the extra rounding is that of the two f16 products.
-//   PV_I8 (default)   the literal reference contraction: v_mfma_i32_32x32x32_i8 on P_i8 x v_i8 (V^T
-//                     operand image vt from qattn_int8_quant_vt), exact int32 per tile, then one
-//                     fused dequantisation per accumulator element and tile, O += acc * sp*sv
-//                     (biased accumulator: 1 VALU per element instead of 2).
-//   Both keep the reference's per-32-key P quantisation; coarser P.V blocks (one dequantisation per
-//   2 or 4 tiles) move O by 1.3e-2 .. 6e-2 from the reference (tools/pv_quant_study.py: the
-//   truncation bias grows with the block), past the 1e-2 bar.  PV_I8 spends 32 packed fp32 FMAs per
-//   wave-tile on the dequantisation but streams half the V bytes (int8 image, 4 KiB per tile through
-//   DMA and LDS instead of 8) and issues 8 MFMAs instead of 12: measured 15-18 % faster than PV_F16
-//   at config 3.
+// Two P_i8 chains.  The fast one above, trunc(127 exp2_f16(f16(S - rm))), equals the reference's
+// trunc(exp2(f16(S - m)) / sp) up to the last bits of the f16 exponential, i.e. it moves P_i8 by one
+// step now and then.  Such a step weighs sp / l of the row: nothing on a row many keys carry, up to
+// |v| / 127 on a row a handful of keys carry (peaked rows).  Tiles that can weigh that much -- some
+// row of the wave has er * LIT_K > l, the tile's weight against the row sum so far, and always the
+// first tile and the causal diagonal tiles -- take the reference's chain literally instead: S
+// rounded in the reference's product order ((X sq) sk) qks, the undeferred running max mt,
+// P = exp2(f16(S - mt)) correctly rounded (exp2_cr), sp = f32(exp2(f16(rm - mt)) / 127) and
+// P_i8 = trunc(P / sp) with the IEEE quotient.  At config 3 about 2 % of the tiles
+// vote literal (tools/fwd_emul.py).
+//
+// P.V (int8:249-250, O += (P_i8 . v_i8) * sp * sv per 32-key tile): the literal contraction,
+// v_mfma_i32_32x32x32_i8 on P_i8 x v_i8 (V^T operand image vt from qattn_int8_quant_vt), exact int32
+// per tile, then one fused dequantisation per accumulator element and tile, O += acc * sp*sv (biased
+// accumulator: 1 VALU per element instead of 2).  Coarser P.V blocks (one dequantisation per 2 or 4
+// tiles) move O by 1.3e-2 .. 6e-2 from the reference (tools/pv_quant_study.py), past the 1e-2 bar.
+// (An f16 P.V form on f16(P_i8 sp) x f16(v_i8 sv) measured 10-15 % slower and was removed in round 5.)
 #include <climits>
 #include <type_traits>
 
@@ -59,11 +59,9 @@ QA_DEVICE int imax3(int a, int b, int c) { return max(max(a, b), c); }
 
 // Per-wave softmax state between the two halves of a tile.
 struct SmTile {
-  v2h d[8];       // f16(S - rm) for the 16 scores of this lane
-  float er;       // exp2(rm - m)
-  float cpv;      // PV_F16: sp = f16(er / 127) (as f32); PV_I8: the tile's dequantisation er/127*sv
-  v2h pi[8];      // CAUSAL diagonal tiles: P_i8 by the reference's literal chain (f16 integers)
-  bool diag;      // (wave-uniform) this tile crosses the wave's causal diagonal
+  v2h d[8];       // f16(S - rm) for the 16 scores of this lane (literal tiles: LitOut::d)
+  float er;       // exp2(rm - m) (0 on literal tiles: their row sum is in l already)
+  float cpv;      // the tile's dequantisation factor sp * sv (in units of the deferred m)
 };
 
 // Shapes: BH = batch * query heads, Sq query and Sk key tokens per head; query head
@@ -72,16 +70,13 @@ struct SmTile {
 // last with the last (bottom-right: new queries against a key/value cache); masked
 // scores are excluded (P = 0).  The reference has neither (its int8 path is square, ungrouped and
 // non-causal, int8:122-127, 344); these are extensions.
-// vop: PV_F16 the vdq image f16 [BHkv*Sk, D]; PV_I8 the vt image (qattn_int8_quant_vt).
-// SPLIT (key-split decoding, PV_I8 non-causal): workgroup (x, y) covers keys [y ks, y ks + ks) of
+// vt: the V^T operand image (qattn_int8_quant_vt).
+// SPLIT (key-split decoding, non-causal): workgroup (x, y) covers keys [y ks, y ks + ks) of
 // its query rows and writes the partial state instead of O: through `out`, opart f16
 // [split][BH*Sq][D] = f16(O_s / l_s) (the split's normalised output); through `lse`, ml f32x2
 // [split][BH*Sq] = {m_s, l_s} (running max, row sum); int8_split_combine_kernel merges the splits.  (The two
 // outputs reuse the pointer arguments and ks the causal offset qoff: the causal instantiations are
 // at the SGPR limit, one more kernel argument pushes their buffer descriptors into VGPRs.)
-// (the causal PV_F16 kernel's diagonal masking does not fit 168 VGPRs: 2 waves per SIMD)
-template <int D, int PV, bool CAUSAL>
-constexpr int fwd_wps() { return CAUSAL ? 2 : Int8FwdCfg<D, PV>::WPS; }
 // Diagnostic build only (-DQA_FWD_STAMP=1, tools/fwd_stamps.py): s_memrealtime stamps (100 MHz) of
 // every workgroup -- entry, end of the prologue, end of the tile loop, exit -- written by lane 0 of
 // wave 0 with vector stores to a buffer of their own that no other code reads.
@@ -93,6 +88,14 @@ constexpr int fwd_wps() { return CAUSAL ? 2 : Int8FwdCfg<D, PV>::WPS; }
 #ifndef QA_FWD_UNROLL
 #define QA_FWD_UNROLL 1
 #endif
+// Diagnostic build only (-DQA_FWD_LIT_COUNT=1, tools/ab_time.py): counts the literal wave-tiles and
+// all wave-tiles (vector atomics by lane 0 of each wave).
+#ifndef QA_FWD_LIT_COUNT
+#define QA_FWD_LIT_COUNT 0
+#endif
+#if QA_FWD_LIT_COUNT
+__device__ unsigned long long g_fwd_lit[2];
+#endif
 #if QA_FWD_STAMP
 __device__ unsigned long long g_fwd_stamp[8192][4];
 #define FWD_STAMP(k)                                                                            \
@@ -103,17 +106,84 @@ __device__ unsigned long long g_fwd_stamp[8192][4];
 #else
 #define FWD_STAMP(k) do { } while (0)
 #endif
-template <int D, int PV, bool CAUSAL, bool SPLIT = false>
-__global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CAUSAL>())) void int8_attn_fwd_kernel(
+// The reference's P_i8 chain for one tile (int8:197-237), literally: S in its product order,
+// next_m = max(mt, rm) with the undeferred running max, P = exp2(f32(f16(S - next_m))) correctly
+// rounded, sp = exp2(f32(f16(rm - next_m))) / 127 (IEEE), P_i8 = trunc(P / sp) with the quotient
+// rounded once (through f64: P * RN(1/sp) is within 2^-52 of P / sp, and a quotient of two floats
+// that is not a rounding midpoint lies at least 2^-49 from one, so the f32 rounding is the IEEE
+// quotient's).  MASK: masked scores (INT_MIN, causal) get P = 0.  acc: the tile's biased S^T
+// accumulator, mx its row max; m: the kernel's deferred running max, the unit of the returned row sum
+// and dequantisation factor.
+// P_i8 leaves as an exponent d = f16(log2(f16(P_i8 / 127 + 0.5 / 127))) that the fast chain's own
+// second half turns back into P_i8 = trunc(127 exp2_f16(d)) (exactly: every P_i8 lands at least
+// 0.42 from both ends of its unit interval, for any rounding of the f16 log2 within one ulp), so the
+// tile loop keeps one SM2 and no second copy of the tile state.
+// (S - next_m is one f16 subtraction here where the reference's eager form rounds through f32 first:
+// the two differ only when that f32 difference is inexact and lands on an f16 midpoint, which needs an
+// odd-integer-spaced difference of operands whose exponents are more than 13 apart -- impossible for
+// f16 operands.)
+struct LitOut {
+  v2h d[8];       // the exponents encoding P_i8
+  float er;       // the tile's row sum (this lane's half), in units of m
+  float cpv;      // sp * sv, in units of m
+  _Float16 mt;    // the running max after the tile
+};
+QA_DEVICE void log2_pk4(const v2h* x, v2h* r) { QA_PK4("v_log_f16"); }
+template <bool MASK>
+QA_DEVICE LitOut literal_chain(const v16i& acc, int mx, float cq, float skt, float svt, float qks,
+                               _Float16 mt, _Float16 m, LdsI8* tab) {
+  LitOut r;
+  const float nkq = -KMAG * cq;                  // exact: sq has 11 significant bits
+  // fl((X + KMAG) sq - KMAG sq) = fl(X sq) (one rounding), then * sk, * qks (int8:200)
+  auto s32 = [&](int a) -> float { return (__builtin_fmaf(__int_as_float(a), cq, nkq) * skt) * qks; };
+  const bool kept = !MASK || mx != INT_MIN;     // the row keeps a key of this tile
+  const _Float16 rmr = (_Float16)s32(mx);        // (rounding is monotone: the max of the S)
+  const _Float16 nmr = (kept && rmr > mt) ? rmr : mt;
+  const float sp = kept ? exp2_cr((_Float16)(rmr - nmr), tab) / 127.0f : 0.f;
+  const double rsp = sp > 0.f ? 1.0 / (double)sp : 0.0;
+  const v2h nm2 = {nmr, nmr};
+  const v2h c1 = {(_Float16)(1.0f / 127.0f), (_Float16)(1.0f / 127.0f)};
+  const v2h c0 = {(_Float16)(0.5f / 127.0f), (_Float16)(0.5f / 127.0f)};
+  float lt = 0.f;
+  v2h w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const v2h x = __builtin_bit_cast(v2h, pk_f16(s32(acc[2 * j]), s32(acc[2 * j + 1]))) - nm2;
+    v2h pi;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float p = exp2_cr(x[e], tab);
+      if (MASK && (acc[2 * j + e] == INT_MIN || !kept)) p = 0.f;
+      lt += p;
+      pi[e] = (_Float16)__builtin_truncf((float)((double)p * rsp));
+    }
+    w[j] = __builtin_elementwise_fma(pi, c1, c0);
+  }
+  log2_pk4(&w[0], &r.d[0]);
+  log2_pk4(&w[4], &r.d[4]);
+  const float wm = kept ? exp2_f32((float)nmr - (float)m) : 0.f;   // next_m units -> m units
+  r.er = lt * wm;
+  r.cpv = (sp * svt) * wm;
+  r.mt = nmr;
+  return r;
+}
+
+// QF (quantise q in the prologue, int8:178-186): q16 holds the fp16 queries; each wave quantises its
+// own 32-row block -- exactly the Q fragment it needs, one lane (row, half) per 64 values, bit-exact
+// with quant_block32_kernel -- and writes q_i8 and sq (the forward's outputs, int8:259-262) and, when
+// qbf is not null, the bf16 image of q_i8 the backward reads.  No separate q pass over HBM.
+template <int D, bool CAUSAL, bool SPLIT = false, bool QF = false>
+__global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
-    const _Float16* __restrict__ sk, const void* __restrict__ vop, const _Float16* __restrict__ sv,
+    const _Float16* __restrict__ sk, const int8_t* __restrict__ vt, const _Float16* __restrict__ sv,
     _Float16* __restrict__ out, _Float16* __restrict__ lse, int BH, int Sq, int Sk, int G, int qoff,
-    float qks) {
-  static_assert(!SPLIT || (PV == PV_I8 && !CAUSAL), "key splits: int8 P.V, non-causal");
-  using C = Int8FwdCfg<D, PV>;
+    float qks, const _Float16* __restrict__ q16, __bf16* __restrict__ qbf) {
+  static_assert(!SPLIT || !CAUSAL, "key splits: non-causal");
+  static_assert(!SPLIT || !QF, "key splits: pre-quantised q");
+  using C = Int8FwdCfg<D>;
   FWD_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // per-tile scales: ck = sk * qks (f32); PV_I8 also sv / 127 (f32)
+  // per-tile scales: ck = sk * qks (f32), sv / 127 (f32)
   float* ck_lds = reinterpret_cast<float*>(smem + C::RING);
 
   const int nq = (Sq + C::QROWS - 1) / C::QROWS;
@@ -134,17 +204,17 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   const int nk = SPLIT ? min(ks, Sk - k0) : Sk;    // its keys
   const long kv_row0 = (long)(bh / G) * Sk + k0;  // its key/value head's rows
   const int8_t* kbase = k_i8 + kv_row0 * D;
-  const void* vbase = PV == PV_F16
-      ? (const void*)(reinterpret_cast<const _Float16*>(vop) + kv_row0 * D)
-      : (const void*)(reinterpret_cast<const int8_t*>(vop) + kv_row0 * D);
+  const int8_t* vbase = vt + kv_row0 * D;
   // causal: key tiles past the workgroup's last query are masked for all of its rows
   const int nt = CAUSAL ? min(Sk / C::KT, (qt * C::QROWS + C::QROWS + qoff + C::KT - 1) / C::KT)
                         : nk / C::KT;
   // per-tile scales, shifted by one tile: entry i holds tile min(i + 1, nt - 1), the tile whose SM1
   // runs in loop iteration i, so that 4 iterations read their scales with one 16-B LDS read
   float* svq_lds = ck_lds + ((nt + 3) & ~3);
+  // the exp2 correction table of the literal chain (exp2_corr.h), after the scale tables
+  unsigned* corr_lds = reinterpret_cast<unsigned*>(svq_lds + ((nt + 3) & ~3));
 
-  DmaPlan<D, PV> dma;
+  DmaPlan<D> dma;
   dma.init(wave, lane, Sk - k0, kbase, vbase);   // (the range bound only: reads stay in nk)
   const unsigned smem_lds = lds_addr(smem);
   dma.issue(smem_lds, 0);
@@ -153,15 +223,51 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   for (int i = tid; i < nt; i += 64 * C::WAVES) {
     const int ti = min(i + 1, nt - 1);
     ck_lds[i] = (float)sk[kv_row0 / 32 + ti] * qks;
-    if constexpr (PV == PV_I8) svq_lds[i] = (float)sv[kv_row0 / 32 + ti] * (1.0f / 127.0f);
+    svq_lds[i] = (float)sv[kv_row0 / 32 + ti] * (1.0f / 127.0f);
   }
+  for (int i = tid; i < EXP2_CORR_WORDS; i += 64 * C::WAVES) corr_lds[i] = g_exp2_corr[i];
   const float ck0 = (float)sk[kv_row0 / 32] * qks;   // tile 0 (the prologue's SM1)
-  const float svq0 = PV == PV_I8 ? (float)sv[kv_row0 / 32] * (1.0f / 127.0f) : 0.f;
+  const float svq0 = (float)sv[kv_row0 / 32] * (1.0f / 127.0f);
 
   // ---- Q fragment (B operand of S^T = K Q^T): lane holds Q[q0+c32][32s + 16h .. +16]
   v4i qf[C::NKS];
   float cq = 0.f;
-  if (active) {
+  if (active && QF) {   // quantise the wave's 32-row block (int8:178-186)
+    const long row = head_row0 + q0 + c32;
+    const _Float16* x16 = q16 + row * D + 16 * h;
+    v8h x[C::NKS][2];
+    float amax = 0.f;
+#pragma unroll
+    for (int s = 0; s < C::NKS; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        x[s][u] = *reinterpret_cast<const v8h*>(x16 + 32 * s + 8 * u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf((float)x[s][u][j]));
+      }
+    amax = wave_max_f(amax);
+    const _Float16 s16 = (_Float16)(amax / 127.0f);
+    cq = (float)s16;
+    const float r = quant_rcp(cq);
+    if (lane == 0) const_cast<_Float16*>(sq)[(head_row0 + q0) / 32] = s16;
+#pragma unroll
+    for (int s = 0; s < C::NKS; ++s) {
+      unsigned w[4];
+      float qv[16];
+      quant8(x[s][0], cq, r, w[0], w[1], qv);
+      quant8(x[s][1], cq, r, w[2], w[3], qv + 8);
+      qf[s] = v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+      *reinterpret_cast<v4i*>(const_cast<int8_t*>(q_i8) + row * D + 32 * s + 16 * h) = qf[s];
+      if (qbf != nullptr) {
+        __bf16* ib = qbf + row * D + 32 * s + 16 * h;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          *reinterpret_cast<v4u*>(ib + 8 * u) =
+              v4u{pk_bf16(qv[8 * u], qv[8 * u + 1]), pk_bf16(qv[8 * u + 2], qv[8 * u + 3]),
+                  pk_bf16(qv[8 * u + 4], qv[8 * u + 5]), pk_bf16(qv[8 * u + 6], qv[8 * u + 7])};
+      }
+    }
+  } else if (active) {
     const int8_t* qrow = q_i8 + (head_row0 + q0 + c32) * D + 16 * h;
 #pragma unroll
     for (int s = 0; s < C::NKS; ++s) qf[s] = *reinterpret_cast<const v4i*>(qrow + 32 * s);
@@ -174,35 +280,24 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   for (int i = 0; i < 16; ++i) kmag[i] = KMAG_BITS;
   asm volatile("" : "+v"(kmag));
 
-  // lane-constant LDS byte offsets: K A-operand chunk (2s+h) of key row c32; PV_F16: V^T A-operand
-  // of d-block b: key rows 4h + (i16>>2) (+16 per k-step, +8 for the 2nd read), columns
-  // 32b + 16gg + 4(i16&3); PV_I8: piece b of the vt image, 16 B per lane
+  // lane-constant LDS byte offsets: K A-operand chunk (2s+h) of key row c32; piece b of the vt
+  // image, 16 B per lane
   int koff[C::NKS], voff[C::NDB];
 #pragma unroll
   for (int s = 0; s < C::NKS; ++s) koff[s] = c32 * D + 16 * ((2 * s + h) ^ k_sw<D>(c32));
-  if constexpr (PV == PV_F16) {
-    const int gg = (lane >> 4) & 1, i16 = lane & 15;
-    const int key_a = 4 * h + (i16 >> 2);
 #pragma unroll
-    for (int b = 0; b < C::NDB; ++b) {
-      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
-      voff[b] = C::K_BYTES + key_a * 2 * D + 16 * ((d / 8) ^ v_sw<D>(key_a)) + (d % 8) * 2;
-    }
-  } else {
-#pragma unroll
-    for (int b = 0; b < C::NDB; ++b) voff[b] = C::K_BYTES + b * 1024 + 16 * lane;
-  }
+  for (int b = 0; b < C::NDB; ++b) voff[b] = C::K_BYTES + b * 1024 + 16 * lane;
 
   v16f o[C::NDB];
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) o[b] = v16f{};
   _Float16 m = (_Float16)(-INFINITY);
   _Float16 m_thr = (_Float16)(-INFINITY);   // m + THR (f16): the deferred running max moves past it
-  _Float16 mt = (_Float16)(-INFINITY);   // CAUSAL: the reference's (undeferred) running max
+  _Float16 mt = (_Float16)(-INFINITY);      // the reference's (undeferred) running max
   float l = 0.f;      // per-lane partial (this lane's key half); the reference's l = 1 is wiped by r = 0
-  float obias = 0.f;  // PV_I8: sum of the tile dequantisation factors (the KMAG bias of O is KMAG * obias)
-  // PV_I8: the dequantisation factor of the tile whose P.V is in flight while SM1 of the next tile
-  // runs; a running-max move there rescales it with O (its int32 product is added after SM1)
+  float obias = 0.f;  // sum of the tile dequantisation factors (the KMAG bias of O is KMAG * obias)
+  // the dequantisation factor of the tile whose P.V is in flight while SM1 of the next tile runs;
+  // a running-max move there rescales it with O (its int32 product is added after SM1)
   float cpv_pend = 0.f;
 
   // ring slot u (the loop below passes compile-time slot numbers: LDS offsets become immediates)
@@ -216,22 +311,52 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     for (int s = 0; s < C::NKS; ++s) kf[s] = *reinterpret_cast<const v4i*>(kl + koff[s]);
   };
   auto qk_mma = [&](const v4i* kf) -> v16i {
-    v16i acc = mfma_i8(kf[0], qf[0], C::QK_BIAS ? kmag : v16i{});
+    v16i acc = mfma_i8(kf[0], qf[0], kmag);
 #pragma unroll
     for (int s = 1; s < C::NKS; ++s) acc = mfma_i8(kf[s], qf[s], acc);
     return acc;
   };
 
-  // first half of the softmax of tile t: row max, d = f16(S - rm), deferred running max, er, and
-  // the tile's P.V scale
+  // O^T += V^T P^T for tile t: operand loads (issued early, consumed after QK(t+1) and SM2(t))
+  // and the MFMAs
+  auto pv_load = [&](int u, v4i* va) {
+    const char* vl = slot_at(u);
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) va[b] = *reinterpret_cast<const v4i*>(vl + voff[b]);
+  };
+  v16i pacc[C::NDB];
+  auto pv_mma = [&](const v4i* va, const v4u* pw) {
+    const v4i p = __builtin_bit_cast(v4i, pw[0]);
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b) pacc[b] = mfma_i8(va[b], p, kmag);
+  };
+  // O += (KMAG + X) * (sp * sv) for the tile's exact int32 X (one fused op per element)
+  auto pv_dequant = [&](float cpv) {
+    // explicit v_pk_fma_f32 pairs (scalar v_fma_f32 measured 2-3 % slower)
+    const v2f_ c2 = {cpv, cpv};
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const v2f_ a = {__int_as_float(pacc[b][r]), __int_as_float(pacc[b][r + 1])};
+        const v2f_ y = __builtin_elementwise_fma(a, c2, v2f_{o[b][r], o[b][r + 1]});
+        o[b][r] = y[0];
+        o[b][r + 1] = y[1];
+      }
+    obias += cpv;
+  };
+
+  // first half of the softmax of tile t: row max, d = f16(S - rm), deferred running max, er, the
+  // tile's P.V scale, and the literal-chain vote
   //   dg (std::true_type / false_type): whether tile t may cross the diagonal (causal), i.e.
-  //   whether the masks and the literal P chain are compiled in
-  auto sm1 = [&](const v16i& acc_in, int t, SmTile& st, float ckt, float svqt, auto dg) {
+  //   whether the masks are compiled in
+  //   pend (std::true_type / false_type): a P.V product is in flight (every SM1 but the prologue's);
+  //   the literal branch adds it to O first, which frees its 64 accumulator registers
+  auto sm1 = [&](const v16i& acc_in, int t, bool live, SmTile& st, float ckt, float svqt, auto dg,
+                 auto pend) {
     // causal tiles crossing this wave's diagonal: keys above the row's query drop out of the max
     // (INT_MIN) and get d = -inf below, so P = 0 and the tile scale ignores them
     const bool diag = CAUSAL && decltype(dg)::value && (t * C::KT + C::KT - 1 > q0 + qoff);
-    // QA_FWD_LITERAL_P: the reference's literal P_i8 chain on every tile (priced)
-    const bool lit = diag || (QA_FWD_LITERAL_P != 0);
     v16i acc = acc_in;
     if (diag) {
       // key > query as one compare per score against an immediate:
@@ -253,51 +378,15 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       auto r = __builtin_amdgcn_permlane32_swap((unsigned)mx, (unsigned)mx, false, false);
       mx = max((int)r[0], (int)r[1]);
     }
-    // S = f16(X * c) (int8:200-203: fp32 products, then fp16)
+    // S = f16(X * c) (int8:200-203: fp32 products, then fp16), on the biased accumulator
     v2h s2[8];
-    _Float16 rm;
-    if constexpr (C::QK_BIAS) {   // on the biased accumulator (QA_FWD_S_PK: packed f32, else fma_mix)
-      const float c = kmag_scale(cq * ckt);
-      const float nb = -KMAG * c;
-#if QA_FWD_S_PK
-      rm = biased_to_f16(mx, c, nb);
-      biased_to_f16x16(acc, c, nb, s2);
-#else
-      rm = fma_mix1(__int_as_float(mx), c, nb);
-      fma_mix16_after(acc, c, nb, mx, s2);
-#endif
-    } else {
-      const float c = cq * ckt;
-      rm = (_Float16)((float)mx * c);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        s2[j] = __builtin_bit_cast(v2h, pk_f16((float)acc[2 * j] * c, (float)acc[2 * j + 1] * c));
-    }
+    const float c = kmag_scale(cq * ckt);
+    const float nb = -KMAG * c;
+    const _Float16 rm = biased_to_f16(mx, c, nb);
+    biased_to_f16x16(acc, c, nb, s2);
     const v2h rm2 = {rm, rm};
 #pragma unroll
     for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;   // f16(S - rm)  (int8:211, 232-236)
-    if constexpr (CAUSAL || QA_FWD_LITERAL_P) {
-      // Diagonal tiles keep few keys per row, where one P_i8 step weighs much in O: there P_i8
-      // follows the reference chain literally (int8:205-237): next_m = max(m, rm) with the
-      // undeferred running max, P = exp2(f32(f16(S - next_m))), sp = exp2(f32(f16(rm - next_m)))/127
-      // and P_i8 = trunc(P / sp), IEEE fp32 divisions.  Other tiles use 127 exp2(f16(S - rm)) (the
-      // same value up to the last bits, which only matter when few keys share the row sum).
-      const bool kept = mx != INT_MIN;     // the row keeps a key of this tile
-      const _Float16 nm_ref = (kept && rm > mt) ? rm : mt;
-      if (kept) mt = nm_ref;
-      st.diag = lit;
-      if (lit) {
-        const float spr = exp2_f32((float)(_Float16)((float)rm - (float)nm_ref)) / 127.0f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const float dr = (float)(_Float16)((float)s2[j][e] - (float)nm_ref);
-            const float pr = __builtin_truncf(exp2_f32(dr) / spr);
-            st.pi[j][e] = (acc[2 * j + e] == INT_MIN || !kept) ? (_Float16)0.0f : (_Float16)pr;
-          }
-      }
-    }
     if (diag) {
       const _Float16 ninf = (_Float16)(-INFINITY);
 #pragma unroll
@@ -315,20 +404,50 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
       m = nm;
       m_thr = m + (_Float16)C::THR;
       l *= r;
-      if constexpr (PV == PV_I8) {
-        obias *= r;
-        cpv_pend *= r;
-      }
+      obias *= r;
+      cpv_pend *= r;
 #pragma unroll
       for (int b = 0; b < C::NDB; ++b) o[b] *= r;
     }
     st.er = exp2_f32((float)(_Float16)(rm - m));
-    if constexpr (PV != PV_I8) st.cpv = (float)(_Float16)(st.er * (1.0f / 127.0f));
-    else st.cpv = st.er * svqt;
+    st.cpv = st.er * svqt;
+    // the vote: the tile can weigh more than 1/LIT_K of the row sum so far (l is this lane's half
+    // of it); the first tile (l = 0) always votes.  Causal diagonal tiles always take the chain.
+    // (`live` is false for the duplicate tile of the loop's last iteration, whose state is never
+    // consumed: the chain adds its row sum to l directly.)
+    bool lit = diag;
+    if constexpr (C::LIT_K > 0) lit = lit || __ballot(st.er * (0.5f * C::LIT_K) > l) != 0;
+    if constexpr (C::LIT_K == 0) lit = true;
+    lit = lit && live;
+#ifdef QA_FWD_LIT_NEVER   // (A/B: the vote and the chain's code, never taken)
+    lit = lit && qks < 0.f;
+#endif
+#if QA_FWD_LIT_COUNT
+    if (lane == 0 && live) {
+      atomicAdd(&g_fwd_lit[1], 1ull);
+      if (lit) atomicAdd(&g_fwd_lit[0], 1ull);
+    }
+#endif
+    if (lit) {
+      asm volatile("" ::: "memory");
+      if constexpr (decltype(pend)::value) {
+        pv_dequant(cpv_pend);
+        cpv_pend = 0.f;   // (the loop's own dequantisation then adds (KMAG + X) * 0)
+      }
+      const LitOut r = literal_chain<CAUSAL>(acc, mx, cq, (float)sk[kv_row0 / 32 + t],
+                                             (float)sv[kv_row0 / 32 + t], qks, mt, m, (LdsI8*)corr_lds);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) st.d[j] = r.d[j];
+      l += r.er;
+      st.er = 0.f;
+      st.cpv = r.cpv;
+      mt = r.mt;
+    } else if (mx != INT_MIN && rm > mt) {
+      mt = rm;
+    }
   };
 
-  // second half: e = exp2(d) (sm2_exp), then l += er * sum e and the P operand (sm2)
-  //   PV_F16: f16(P_i8 * sp) as 2 x 4 packed dwords; PV_I8: the 16 P_i8 bytes
+  // second half: e = exp2(d) (sm2_exp), then l += er * sum e and the 16 P_i8 bytes (sm2)
   auto sm2_exp = [&](const SmTile& st, v2h* e) {
     exp2_pk4(&st.d[0], &e[0]);
     exp2_pk4(&st.d[4], &e[4]);
@@ -337,89 +456,10 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     // row sum of e: packed f16 adds (pairs, then sums of 4 and 8 values <= 8), one f32 mix-add
     const v2h s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
     l = fmaf(pk_hsum(s), st.er, l);
-    if ((CAUSAL || QA_FWD_LITERAL_P) && st.diag) {   // the literal-chain P_i8 of the tile (sm1)
-      if constexpr (PV != PV_I8) {
-        const _Float16 sp = (_Float16)st.cpv;
-        const v2h sp2 = {sp, sp};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pw[j / 4][j % 4] = __builtin_bit_cast(unsigned, st.pi[j] * sp2);
-      } else {
-        const v2h k1024 = {(_Float16)1024.0f, (_Float16)1024.0f};
-        unsigned y[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = __builtin_bit_cast(unsigned, st.pi[j] + k1024);
-        pw[0] = __builtin_bit_cast(v4u, pack_p_index(y));
-      }
-      return;
-    }
-    if constexpr (PV != PV_I8) {
-      const _Float16 sp = (_Float16)st.cpv;
-      const v2h sp2 = {sp, sp};
-      const _Float16 nsp = (_Float16)(-1024.0f) * sp;
-      const v2h nsp2 = {nsp, nsp};
-      v2h w[8];
-      p_operand8(e, sp2, nsp2, w);
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pw[u][j] = __builtin_bit_cast(unsigned, w[4 * u + j]);
-    } else {
-      const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
-      unsigned y[8];
-      p_index8(e, k127, y);
-      pw[0] = __builtin_bit_cast(v4u, pack_p_index(y));
-    }
-  };
-
-  // O^T += V^T P^T for tile t: operand loads (issued early, consumed after QK(t+1) and SM2(t))
-  // and the MFMAs
-  using VFrag = typename std::conditional<PV != PV_I8, v8h, v4i>::type;
-  constexpr int NVF = PV != PV_I8 ? 2 * C::NDB : C::NDB;
-  auto pv_load = [&](int u, VFrag* va) {
-    const char* vl = slot_at(u);
-    if constexpr (PV == PV_F16) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int b = 0; b < C::NDB; ++b) {
-          const char* a = vl + voff[b] + 16 * s * 2 * D;
-          va[s * C::NDB + b] = __builtin_bit_cast(v8h, ds_read_tr16_x2(a, a + 8 * 2 * D));
-        }
-    } else {
-#pragma unroll
-      for (int b = 0; b < C::NDB; ++b) va[b] = *reinterpret_cast<const v4i*>(vl + voff[b]);
-    }
-  };
-  v16i pacc[PV == PV_I8 ? C::NDB : 1];
-  auto pv_mma = [&](const VFrag* va, const v4u* pw) {
-    if constexpr (PV != PV_I8) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int b = 0; b < C::NDB; ++b)
-          o[b] = mfma_f16(va[s * C::NDB + b], __builtin_bit_cast(v8h, pw[s]), o[b]);
-    } else {
-      const v4i p = __builtin_bit_cast(v4i, pw[0]);
-#pragma unroll
-      for (int b = 0; b < C::NDB; ++b) pacc[b] = mfma_i8(va[b], p, kmag);
-    }
-  };
-  // PV_I8: O += (KMAG + X) * (sp * sv) for the tile's exact int32 X (one fused op per element)
-  auto pv_dequant = [&](float cpv) {
-    if constexpr (PV == PV_I8) {
-      // explicit v_pk_fma_f32 pairs (scalar v_fma_f32 measured 2-3 % slower)
-      const v2f_ c2 = {cpv, cpv};
-#pragma unroll
-      for (int b = 0; b < C::NDB; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const v2f_ a = {__int_as_float(pacc[b][r]), __int_as_float(pacc[b][r + 1])};
-          const v2f_ y = __builtin_elementwise_fma(a, c2, v2f_{o[b][r], o[b][r + 1]});
-          o[b][r] = y[0];
-          o[b][r + 1] = y[1];
-        }
-      obias += cpv;
-    }
+    const v2h k127 = {(_Float16)127.0f, (_Float16)127.0f};
+    unsigned y[8];
+    p_index8(e, k127, y);
+    pw[0] = __builtin_bit_cast(v4u, pack_p_index(y));
   };
 
   vmem_drain();
@@ -429,7 +469,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   SmTile st;
   // One loop iteration per tile t: SM2 and P.V of tile t, QK and SM1 of tile t+1.  The last iteration
   // computes QK / SM1 of a duplicate of the last tile (its slot holds a clamped re-load): harmless
-  // (its row max cannot move m) and it keeps the loop body branch-free.
+  // (its row max cannot move m, and its state is never used) and it keeps the loop body branch-free.
   //   cur, nxt: ring slots of tiles t and t+1; fill: the slot the DMA of tile t+3 goes to (freed by
   //   the barrier); ckn, svqn: the scales of tile t+1
   auto iter = [&](int t, int cur, int nxt, int fill, float ckn, float svqn, auto dg) {
@@ -441,52 +481,50 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
     const int tn = min(t + 1, nt - 1);
     v4i kf[C::NKS];
     qk_load(nxt, kf);
-    VFrag va[NVF];
+    v4i va[C::NDB];
     pv_load(cur, va);
     v2h e[8];
     sm2_exp(st, e);
     __builtin_amdgcn_sched_barrier(0);
     const v16i nacc = qk_mma(kf);
     __builtin_amdgcn_sched_barrier(0);
-    v4u pw[2];
+    v4u pw[1];
     sm2(st, e, pw);
     cpv_pend = st.cpv;
     pv_mma(va, pw);
-    sm1(nacc, tn, st, ckn, svqn, dg);   // (may rescale O, obias and cpv_pend)
-    pv_dequant(cpv_pend);   // PV_I8: after SM1(t+1), so the PV MFMAs of tile t have retired
+    sm1(nacc, tn, t + 1 < nt, st, ckn, svqn, dg, std::true_type{});   // (may rescale O, obias, cpv_pend)
+    pv_dequant(cpv_pend);   // after SM1(t+1), so the PV MFMAs of tile t have retired
   };
   if (active) {
     {
       v4i kf[C::NKS];
       qk_load(0, kf);
-      sm1(qk_mma(kf), 0, st, ck0, svq0, std::true_type{});
+      sm1(qk_mma(kf), 0, true, st, ck0, svq0, std::true_type{}, std::false_type{});
     }
     // Causal: iteration t runs SM1 of tile t+1, and tiles below td0 = (first query of the workgroup
-    // + qoff) / KT cross no wave's diagonal, so iterations t < td0 - 1 run with the masks and the
-    // literal P chain compiled out (the same values: nothing is masked there) and the rest, at
-    // most WAVES + 1 of them, with them.
+    // + qoff) / KT cross no wave's diagonal, so iterations t < td0 - 1 run with the masks compiled
+    // out (the same values: nothing is masked there) and the rest, at most WAVES + 1 of them, with
+    // them.
     const int tmain = CAUSAL ? max(0, min(nt, (qt * C::QROWS + qoff) / C::KT - 1)) : nt;
     // groups of NSLOT = 4 tiles with compile-time ring slots (immediate LDS offsets, one 16-B read
-    // of each scale table per group), then the remaining tiles with run-time slots.  Only where the
-    // unrolled body fits the register budget (the 3-wave f16 P.V kernel spills with it).
+    // of each scale table per group), then the remaining tiles with run-time slots
     static_assert(C::NSLOT == 4, "ring of 4 slots");
-    constexpr bool UNROLL = PV == PV_I8 && QA_FWD_UNROLL;
+    constexpr bool UNROLL = QA_FWD_UNROLL && !CAUSAL;
     const std::false_type nodiag{};
     int t = 0;
     for (; UNROLL && t + 4 <= tmain; t += 4) {
       const v4f ck4 = *reinterpret_cast<const v4f*>(ck_lds + t);
-      const v4f sv4 = PV == PV_I8 ? *reinterpret_cast<const v4f*>(svq_lds + t) : v4f{};
+      const v4f sv4 = *reinterpret_cast<const v4f*>(svq_lds + t);
       iter(t, 0, 1, 3, ck4[0], sv4[0], nodiag);
       iter(t + 1, 1, 2, 0, ck4[1], sv4[1], nodiag);
       iter(t + 2, 2, 3, 1, ck4[2], sv4[2], nodiag);
       iter(t + 3, 3, 0, 2, ck4[3], sv4[3], nodiag);
     }
     for (; t < tmain; ++t)
-      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], PV == PV_I8 ? svq_lds[t] : 0.f, nodiag);
+      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], nodiag);
     if constexpr (CAUSAL) {
       for (; t < nt; ++t)
-        iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], PV == PV_I8 ? svq_lds[t] : 0.f,
-             std::true_type{});
+        iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], std::true_type{});
     }
   } else {   // a wave past the last query row: the barriers and the ring's DMA only
     for (int t = 0; t < nt; ++t) {
@@ -513,26 +551,28 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D, PV>::WAVES), (fwd_wps<D, PV, CA
   const long qrow = head_row0 + q0 + c32;
   if (h == 0) lse[qrow] = (_Float16)((float)m + (float)(_Float16)log2_f32(l));
   const float inv = 1.0f / l;
-  store_rows<D, _Float16, 1, PV == PV_I8>(o, inv, smem + wave * RowTile<D, _Float16>::BYTES,
-                                          out + (head_row0 + q0) * D, lane, -KMAG * obias * inv);
+  store_rows<D, _Float16, 1, true>(o, inv, smem + wave * RowTile<D, _Float16>::BYTES,
+                                   out + (head_row0 + q0) * D, lane, -KMAG * obias * inv);
 #if QA_FWD_STAMP
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   FWD_STAMP(3);
 #endif
 }
 
-template <int D, int PV, bool CAUSAL>
+template <int D, bool CAUSAL, bool QF>
 static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                      const void* vop, const void* sv, void* out, void* lse, long bh, long sq_tok,
-                      long sk_tok, int group, int qoff, float qks, hipStream_t st) {
-  using C = Int8FwdCfg<D, PV>;
+                      const void* vt, const void* sv, void* out, void* lse, long bh, long sq_tok,
+                      long sk_tok, int group, int qoff, float qks, const void* q16, void* qbf,
+                      hipStream_t st) {
+  using C = Int8FwdCfg<D>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
-  const int lds = C::RING + (int)((((sk_tok / 32) + 3) / 4 * 4) * 4 * (PV == PV_I8 ? 2 : 1));
-  { static int granted_ = 0; lds_grant((const void*)int8_attn_fwd_kernel<D, PV, CAUSAL>, lds, granted_); }
-  hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV, CAUSAL>), dim3((unsigned)(nq * bh)),
-                     dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
-                     (const int8_t*)k_i8, (const _Float16*)sk, vop, (const _Float16*)sv,
-                     (_Float16*)out, (_Float16*)lse, (int)bh, (int)sq_tok, (int)sk_tok, group, qoff, qks);
+  const int lds = C::lds_bytes((int)(sk_tok / 32));
+  auto kern = int8_attn_fwd_kernel<D, CAUSAL, false, QF>;
+  { static int granted_ = 0; if (!lds_grant((const void*)kern, lds, granted_)) return 1; }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds, st,
+                     (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
+                     (const int8_t*)vt, (const _Float16*)sv, (_Float16*)out, (_Float16*)lse, (int)bh,
+                     (int)sq_tok, (int)sk_tok, group, qoff, qks, (const _Float16*)q16, (__bf16*)qbf);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -573,26 +613,30 @@ template <int D>
 static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
                             const void* vt, const void* sv, void* opart, void* ml, long bh, long sq_tok,
                             long sk_tok, int group, int ks, float qks, hipStream_t st) {
-  using C = Int8FwdCfg<D, PV_I8>;
+  using C = Int8FwdCfg<D>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int nsplit = (int)((sk_tok + ks - 1) / ks);
-  const int lds = C::RING + (int)((((ks / 32) + 3) / 4 * 4) * 8);
-  { static int granted_ = 0; lds_grant((const void*)int8_attn_fwd_kernel<D, PV_I8, false, true>, lds, granted_); }
-  hipLaunchKernelGGL((int8_attn_fwd_kernel<D, PV_I8, false, true>), dim3((unsigned)(nq * bh), (unsigned)nsplit),
+  const int lds = C::lds_bytes(ks / 32);
+  { static int granted_ = 0; if (!lds_grant((const void*)int8_attn_fwd_kernel<D, false, true>, lds, granted_)) return 1; }
+  hipLaunchKernelGGL((int8_attn_fwd_kernel<D, false, true>), dim3((unsigned)(nq * bh), (unsigned)nsplit),
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
-                     (const int8_t*)k_i8, (const _Float16*)sk, vt, (const _Float16*)sv, (_Float16*)opart,
-                     (_Float16*)ml, (int)bh, (int)sq_tok, (int)sk_tok, group, ks, qks);
+                     (const int8_t*)k_i8, (const _Float16*)sk, (const int8_t*)vt, (const _Float16*)sv,
+                     (_Float16*)opart, (_Float16*)ml, (int)bh, (int)sq_tok, (int)sk_tok, group, ks, qks,
+                     nullptr, nullptr);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-template <int PV>
+// q16 != nullptr: quantise q in the attention kernel (QF), writing q_i8, sq and (qbf != nullptr)
+// the bf16 image
 static int fwd_dispatch(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                        const void* vop, const void* sv, void* out, void* lse, long bh, long sq_tok,
-                        long sk_tok, int group, int causal, int head_dim, float qks, void* stream) {
+                        const void* vt, const void* sv, void* out, void* lse, long bh, long sq_tok,
+                        long sk_tok, int group, int causal, int head_dim, float qks, const void* q16,
+                        void* qbf, void* stream) {
   if (sq_tok % 32 != 0 || sk_tok % 32 != 0 || group < 1 || bh % group != 0 ||
       (head_dim != 64 && head_dim != 128) || causal < 0 || causal > 2)
     return 1;
   if (bh == 0 || sq_tok == 0) return 0;
+  if (sv == nullptr) return 1;
   if (sk_tok == 0 || (causal == 2 && sk_tok < sq_tok)) return 1;   // every query keeps a key
   const int qoff = causal == 2 ? (int)(sk_tok - sq_tok) : 0;
   hipStream_t st = (hipStream_t)stream;
@@ -600,15 +644,20 @@ static int fwd_dispatch(const void* q_i8, const void* sq, const void* k_i8, cons
   // consecutive [sq_tok, D] blocks (rows, scale blocks, O and lse alike), so they run as one virtual
   // head of group * sq_tok rows against their key/value head -- the same arithmetic per row
   // (bit-identical), with the workgroup's waves filled and each key/value tile read once per group.
-  if (causal == 0 && group > 1 && sq_tok % Int8FwdCfg<128, PV>::QROWS != 0) {
+  if (causal == 0 && group > 1 && sq_tok % Int8FwdCfg<128>::QROWS != 0) {
     sq_tok *= group;
     bh /= group;
     group = 1;
   }
-#define QA_L(Dv, CV) \
-  launch_fwd<Dv, PV, CV>(q_i8, sq, k_i8, sk, vop, sv, out, lse, bh, sq_tok, sk_tok, group, qoff, qks, st)
-  if (head_dim == 128) return causal ? QA_L(128, true) : QA_L(128, false);
-  return causal ? QA_L(64, true) : QA_L(64, false);
+#define QA_L(Dv, CV, QV) \
+  launch_fwd<Dv, CV, QV>(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, qoff, qks, \
+                         q16, qbf, st)
+  if (q16 != nullptr) {
+    if (head_dim == 128) return causal ? QA_L(128, true, true) : QA_L(128, false, true);
+    return causal ? QA_L(64, true, true) : QA_L(64, false, true);
+  }
+  if (head_dim == 128) return causal ? QA_L(128, true, false) : QA_L(128, false, false);
+  return causal ? QA_L(64, true, false) : QA_L(64, false, false);
 #undef QA_L
 }
 
@@ -616,6 +665,11 @@ static int fwd_dispatch(const void* q_i8, const void* sq, const void* k_i8, cons
 
 using namespace qattn;
 
+#if QA_FWD_LIT_COUNT
+extern "C" int qattn_fwd_lit_count(void* host_dst) {
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(qattn::g_fwd_lit), sizeof(qattn::g_fwd_lit)) == hipSuccess ? 0 : 2;
+}
+#endif
 #if QA_FWD_STAMP
 extern "C" int qattn_fwd_stamps(void* host_dst) {
   return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(qattn::g_fwd_stamp), sizeof(qattn::g_fwd_stamp)) == hipSuccess ? 0 : 2;
@@ -623,31 +677,31 @@ extern "C" int qattn_fwd_stamps(void* host_dst) {
 #endif
 
 extern "C" int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const void* k_i8,
-                                      const void* sk, const void* vdq, void* out, void* lse, long bh,
-                                      long sq_tok, long sk_tok, int group, int causal, int head_dim,
-                                      float qks, void* stream) {
-  return fwd_dispatch<PV_F16>(q_i8, sq, k_i8, sk, vdq, nullptr, out, lse, bh, sq_tok, sk_tok, group,
-                              causal, head_dim, qks, stream);
+                                      const void* sk, const void* vt, const void* sv, void* out,
+                                      void* lse, long bh, long sq_tok, long sk_tok, int group,
+                                      int causal, int head_dim, float qks, void* stream) {
+  return fwd_dispatch(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, causal,
+                      head_dim, qks, nullptr, nullptr, stream);
+}
+
+extern "C" int qattn_int8_attn_fwd_qf(const void* q, void* q_i8, void* sq, void* q_bf, const void* k_i8,
+                                      const void* sk, const void* vt, const void* sv, void* out,
+                                      void* lse, long bh, long sq_tok, long sk_tok, int group,
+                                      int causal, int head_dim, float qks, void* stream) {
+  if (q == nullptr || q_i8 == nullptr || sq == nullptr) return 1;
+  return fwd_dispatch(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, causal,
+                      head_dim, qks, q, q_bf, stream);
 }
 
 extern "C" int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
-                                   const void* vdq, void* out, void* lse, long bh, long seq,
-                                   int head_dim, float qks, void* stream) {
-  return qattn_int8_attn_fwd_ex(q_i8, sq, k_i8, sk, vdq, out, lse, bh, seq, seq, 1, 0, head_dim, qks,
-                                stream);
+                                   const void* vt, const void* sv, void* out, void* lse, long bh,
+                                   long seq, int head_dim, float qks, void* stream) {
+  return qattn_int8_attn_fwd_ex(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, seq, seq, 1, 0, head_dim,
+                                qks, stream);
 }
 
-extern "C" int qattn_int8_attn_fwd_i8pv_ex(const void* q_i8, const void* sq, const void* k_i8,
-                                           const void* sk, const void* vt, const void* sv, void* out,
-                                           void* lse, long bh, long sq_tok, long sk_tok, int group,
-                                           int causal, int head_dim, float qks, void* stream) {
-  if (sv == nullptr && bh > 0 && sq_tok > 0) return 1;   // (empty problems: nothing to read)
-  return fwd_dispatch<PV_I8>(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, causal,
-                             head_dim, qks, stream);
-}
-
-// Key-split (flash-decoding) form of qattn_int8_attn_fwd_i8pv_ex for short query blocks against
-// long key ranges (the int8 key/value cache), non-causal: every workgroup covers
+// Key-split (flash-decoding) form of qattn_int8_attn_fwd_ex for short query blocks against long
+// key ranges (the int8 key/value cache), non-causal: every workgroup covers
 // keys_per_split keys (a multiple of 32) of its query rows and writes the partial state
 //   opart f16 [nsplit][bh*sq_tok][D] = O_s / l_s and ml f32x2 [nsplit][bh*sq_tok] = {m_s, l_s},
 // nsplit = ceil(sk_tok / keys_per_split); qattn_int8_split_combine merges it into out / lse.

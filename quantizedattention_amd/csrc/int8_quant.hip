@@ -19,15 +19,12 @@ namespace qattn {
 // DEQ: also write f16(idx * s) (the forward's P.V operand for v); IMG: also write bf16(idx) (the
 // exact transposed-read image the backward's accumulating products use for q and k).
 template <int D, bool DEQ, bool SMOOTH, bool IMG>
-__global__ __launch_bounds__(256) void quant_block32_kernel(
-    const _Float16* __restrict__ x, int8_t* __restrict__ idx, _Float16* __restrict__ scale,
-    _Float16* __restrict__ deq, __bf16* __restrict__ img, const _Float16* __restrict__ kmean,
-    long nblocks, int rows_per_head) {
+QA_DEVICE void quant_block32(const _Float16* __restrict__ x, int8_t* __restrict__ idx,
+                             _Float16* __restrict__ scale, _Float16* __restrict__ deq,
+                             __bf16* __restrict__ img, const _Float16* __restrict__ kmean,
+                             long blk, int rows_per_head, int lane) {
   constexpr int ELEMS = 32 * D;        // elements per block
   constexpr int ITERS = ELEMS / 512;   // 8 halfs per lane per iteration
-  const int lane = threadIdx.x & 63;
-  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blk >= nblocks) return;
   const _Float16* xb = x + blk * ELEMS;
   v8h v[ITERS];
   const _Float16* km = nullptr;
@@ -71,24 +68,30 @@ __global__ __launch_bounds__(256) void quant_block32_kernel(
     }
   }
 }
+template <int D, bool DEQ, bool SMOOTH, bool IMG>
+__global__ __launch_bounds__(256) void quant_block32_kernel(
+    const _Float16* __restrict__ x, int8_t* __restrict__ idx, _Float16* __restrict__ scale,
+    _Float16* __restrict__ deq, __bf16* __restrict__ img, const _Float16* __restrict__ kmean,
+    long nblocks, int rows_per_head) {
+  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= nblocks) return;
+  quant_block32<D, DEQ, SMOOTH, IMG>(x, idx, scale, deq, img, kmean, blk, rows_per_head,
+                                     threadIdx.x & 63);
+}
 
 // ------------------------------------------------------------ V with the int8 P.V operand image
 // One wave per 32-row block of v: the reference quantiser (v_i8 row-major + sv, bit-exact as above)
 // and, of the same indices, the V^T operand image vt of the forward's int8 P.V product
-// (qattn_int8_attn_fwd_i8pv_ex): per block D/32 pieces of 1 KiB; piece b holds for lane
+// (qattn_int8_attn_fwd_ex): per block D/32 pieces of 1 KiB; piece b holds for lane
 // L = 32h + c the 16 bytes v_i8[key pi(h, j)][32b + c], j = 0..15, pi(h, j) = (j & 3) + 8(j >> 2) + 4h
 // -- the A operand of v_mfma_i32_32x32x32_i8 for V^T in the key order of the S^T accumulator
 // (common.h).  Lane (row c, half h) loads v[c][32b + 16h .. +16]: exactly the A operand of the
 // block in natural order, which one i8 MFMA against the identity transposes into that image.
 template <int D>
-__global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restrict__ v,
-                                                       int8_t* __restrict__ vi,
-                                                       _Float16* __restrict__ sv,
-                                                       int8_t* __restrict__ vt, long nblocks) {
+QA_DEVICE void quant_vt(const _Float16* __restrict__ v, int8_t* __restrict__ vi,
+                        _Float16* __restrict__ sv, int8_t* __restrict__ vt, long blk, int lane) {
   constexpr int NDB = D / 32;
-  const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
-  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blk >= nblocks) return;
+  const int h = lane >> 5, c = lane & 31;
   const long row = blk * 32 + c;
   v8h x[NDB][2];
   float amax = 0.f;
@@ -117,6 +120,34 @@ __global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restric
     const v16i t = mfma_i8(a, ident, v16i{});
     *reinterpret_cast<v4i*>(vt + blk * 32 * D + b * 1024 + 16 * lane) = pack_acc_bytes(t);
   }
+}
+template <int D>
+__global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restrict__ v,
+                                                       int8_t* __restrict__ vi,
+                                                       _Float16* __restrict__ sv,
+                                                       int8_t* __restrict__ vt, long nblocks) {
+  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= nblocks) return;
+  quant_vt<D>(v, vi, sv, vt, blk, threadIdx.x & 63);
+}
+// k and v of one forward in one launch: workgroups alternate between 4 k blocks (the quantiser,
+// with the k-mean smoothing and the backward's bf16 image as asked) and 4 v blocks (v_i8, sv and the
+// P.V operand image), so the two streams share the machine from the first to the last wave and pay
+// one launch ramp instead of two.
+template <int D, bool SMOOTH, bool IMG>
+__global__ __launch_bounds__(256) void quant_kv_kernel(
+    const _Float16* __restrict__ k, int8_t* __restrict__ ki, _Float16* __restrict__ sk,
+    __bf16* __restrict__ kimg, const _Float16* __restrict__ kmean, const _Float16* __restrict__ v,
+    int8_t* __restrict__ vi, _Float16* __restrict__ sv, int8_t* __restrict__ vt, long nblocks,
+    int rows_per_head) {
+  const long wg = blockIdx.x >> 1;
+  const long blk = wg * 4 + (threadIdx.x >> 6);
+  if (blk >= nblocks) return;
+  if (blockIdx.x & 1)
+    quant_vt<D>(v, vi, sv, vt, blk, threadIdx.x & 63);
+  else
+    quant_block32<D, false, SMOOTH, IMG>(k, ki, sk, nullptr, kimg, kmean, blk, rows_per_head,
+                                         threadIdx.x & 63);
 }
 // vt from stored indices (an int8 key/value cache restored from its wire format, kv_cache.py)
 template <int D>
@@ -231,6 +262,29 @@ extern "C" int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt
   else
     hipLaunchKernelGGL(quant_vt_kernel<64>, grid, block, 0, st, (const _Float16*)v, (int8_t*)v_i8,
                        (_Float16*)sv, (int8_t*)vt, nblocks);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_int8_quant_kv(const void* k, void* k_i8, void* sk, void* k_img, const void* kmean,
+                                   const void* v, void* v_i8, void* sv, void* vt, long rows,
+                                   int rows_per_head, int head_dim, void* stream) {
+  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  if (kmean && rows_per_head % 32 != 0) return 1;
+  const long nblocks = rows / 32;
+  if (nblocks == 0) return 0;
+  dim3 grid((unsigned)(2 * ((nblocks + 3) / 4))), block(256);
+  hipStream_t st = (hipStream_t)stream;
+#define QA_KV(Dv, SM, IM)                                                                          \
+  hipLaunchKernelGGL((quant_kv_kernel<Dv, SM, IM>), grid, block, 0, st, (const _Float16*)k,        \
+                     (int8_t*)k_i8, (_Float16*)sk, (__bf16*)k_img, (const _Float16*)kmean,          \
+                     (const _Float16*)v, (int8_t*)v_i8, (_Float16*)sv, (int8_t*)vt, nblocks,        \
+                     rows_per_head)
+#define QA_KV_D(Dv)                                                                                \
+  if (kmean) { if (k_img) QA_KV(Dv, true, true); else QA_KV(Dv, true, false); }                   \
+  else { if (k_img) QA_KV(Dv, false, true); else QA_KV(Dv, false, false); }
+  if (head_dim == 128) { QA_KV_D(128) } else { QA_KV_D(64) }
+#undef QA_KV_D
+#undef QA_KV
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -12,7 +12,7 @@
 //
 // Schemas (reference file:line of the computation each replaces):
 //   int8_quant(Tensor x, int block) -> (Tensor, Tensor)                 attention_int8.py:178-186
-//   int8_fwd(Tensor q, Tensor k, Tensor v, bool smooth, bool causal, str pv)  attention_int8.py:20-65, 97-262
+//   int8_fwd(Tensor q, Tensor k, Tensor v, bool smooth, bool causal)   attention_int8.py:20-65, 97-262
 //       -> (O, lse, q_i8, k_i8, v_i8, sq, sk, sv)        (k_i8 row-major [B*Hkv*Sk, D])
 //   int8_bwd(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, bool causal, int kv_heads)
 //       -> (dq, dk, dv)                                                  attention_int8.py:264-432
@@ -27,8 +27,12 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <c10/hip/HIPCachingAllocator.h>
+
 #include <cmath>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 
@@ -72,10 +76,36 @@ Tensor empty(at::IntArrayRef shape, at::ScalarType dt, const Tensor& like) {
   return at::empty(shape, like.options().dtype(dt));
 }
 
-Tensor try_empty(int64_t bytes, const Tensor& like) {   // undefined when the allocator refuses
+// A backward workspace of `bytes`, undefined when the allocator refuses.  torch's caching allocator
+// frees every cached block and retries before it raises, so after one refusal a workspace that large
+// is tried again only when the device has room for it (hipMemGetInfo free bytes plus the allocator's
+// reserved-but-unused bytes): a training loop whose workspace never fits does not flush the cache in
+// every backward (the same rule as _lib.try_workspace).
+Tensor try_empty(int64_t bytes, const Tensor& like) {
+  static std::mutex mu;
+  static std::map<int, int64_t> refused;   // device -> smallest refused size
+  const int dev = like.device().index();
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = refused.find(dev);
+    if (it != refused.end() && bytes >= it->second) {
+      size_t free_b = 0, total_b = 0;
+      const auto st = c10::hip::HIPCachingAllocator::getDeviceStats(dev);
+      const int64_t spare = st.reserved_bytes[0].current - st.allocated_bytes[0].current;
+      if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || (int64_t)free_b + spare < bytes)
+        return Tensor();
+    }
+  }
   try {
-    return at::empty({bytes}, like.options().dtype(at::kByte));
+    Tensor t = at::empty({bytes}, like.options().dtype(at::kByte));
+    std::lock_guard<std::mutex> g(mu);
+    auto it = refused.find(dev);
+    if (it != refused.end() && bytes >= it->second) refused.erase(it);
+    return t;
   } catch (const c10::OutOfMemoryError&) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = refused.find(dev);
+    if (it == refused.end() || bytes < it->second) refused[dev] = bytes;
     return Tensor();
   }
 }
@@ -112,10 +142,8 @@ void check_int8(const Tensor& q, const Tensor& k, const Tensor& v) {
 
 using T8 = std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor>;
 
-// attention_int8._int8_forward.  pv: the P.V mode, as attention_int8.PV_MODES ("i8", "f16";
-// ops.int8_fwd passes attention_int8.PV_MODE); "" = QATTN_INT8_PV, else "i8".
-T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smooth, bool causal,
-            c10::string_view pv_in) {
+// attention_int8._int8_forward
+T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smooth, bool causal) {
   check_int8(q_in, k_in, v_in);
   require_gpu({&q_in, &k_in, &v_in});
   Ctx c(q_in);
@@ -123,19 +151,11 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
                v = v_in.to(at::kHalf).contiguous();
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
   const int64_t Hkv = k.size(1), Sk = k.size(2), N = B * H * S, Nkv = B * Hkv * Sk;
-  std::string pv(pv_in.data(), pv_in.size());
-  if (pv.empty()) {
-    const char* e = std::getenv("QATTN_INT8_PV");
-    pv = (e && *e) ? e : "i8";
-  }
-  TORCH_CHECK_VALUE(pv == "i8" || pv == "f16", "qattn int8: unknown P.V mode '", pv,
-                    "' (one of i8, f16)");
-  const bool f16pv = pv != "i8";
   Tensor q_i8 = empty({N, D}, at::kChar, q), k_i8 = empty({Nkv, D}, at::kChar, q),
          v_i8 = empty({Nkv, D}, at::kChar, q);
   Tensor sq = empty({N / 32}, at::kHalf, q), sk = empty({Nkv / 32}, at::kHalf, q),
          sv = empty({Nkv / 32}, at::kHalf, q);
-  Tensor vop = empty({Nkv, D}, f16pv ? at::kHalf : at::kChar, q);
+  Tensor vt = empty({Nkv, D}, at::kChar, q);   // the int8 V^T operand image
   Tensor O = empty({B, H, S, D}, at::kHalf, q), lse = empty({N}, at::kHalf, q);
   Tensor k_mean;
   if (N == 0 || Nkv == 0) {   // an empty problem: nothing to read, zero outputs
@@ -147,24 +167,14 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
     k_mean = empty({B, Hkv, 1, D}, at::kHalf, q);
     call(qattn_kmean(P(k), P(k_mean), B * Hkv, Sk, (int)D, c.stream), "kmean");
   }
-  call(qattn_int8_quant_img(P(q), P(q_i8), P(sq), nullptr, nullptr, nullptr, N, (int)S, (int)D, c.stream),
-       "quantise q");
-  call(qattn_int8_quant_img(P(k), P(k_i8), P(sk), nullptr, nullptr, P(k_mean), Nkv, (int)Sk, (int)D,
-                            c.stream),
-       "quantise k");
+
   const float qks = qk_scale(D);
-  if (f16pv) {
-    call(qattn_int8_quant(P(v), P(v_i8), P(sv), P(vop), nullptr, Nkv, (int)Sk, (int)D, c.stream),
-         "quantise v");
-    call(qattn_int8_attn_fwd_ex(P(q_i8), P(sq), P(k_i8), P(sk), P(vop), P(O), P(lse), B * H, S, Sk,
-                                (int)(H / Hkv), causal ? 1 : 0, (int)D, qks, c.stream),
-         "int8 forward");
-  } else {
-    call(qattn_int8_quant_vt(P(v), P(v_i8), P(sv), P(vop), Nkv, (int)D, c.stream), "quantise v");
-    call(qattn_int8_attn_fwd_i8pv_ex(P(q_i8), P(sq), P(k_i8), P(sk), P(vop), P(sv), P(O), P(lse), B * H,
-                                     S, Sk, (int)(H / Hkv), causal ? 1 : 0, (int)D, qks, c.stream),
-         "int8 forward");
-  }
+  call(qattn_int8_quant_kv(P(k), P(k_i8), P(sk), nullptr, P(k_mean), P(v), P(v_i8), P(sv), P(vt), Nkv,
+                           (int)Sk, (int)D, c.stream),
+       "quantise k, v");
+  call(qattn_int8_attn_fwd_qf(P(q), P(q_i8), P(sq), nullptr, P(k_i8), P(sk), P(vt), P(sv), P(O), P(lse),
+                              B * H, S, Sk, (int)(H / Hkv), causal ? 1 : 0, (int)D, qks, c.stream),
+       "int8 forward");
   return {O, lse, q_i8, k_i8, v_i8, sq, sk, sv};
 }
 
@@ -389,7 +399,7 @@ Tensor mxfp4_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in) {
 
 TORCH_LIBRARY(qattn, m) {
   m.def("int8_quant(Tensor x, int block) -> (Tensor, Tensor)");
-  m.def("int8_fwd(Tensor q, Tensor k, Tensor v, bool smooth, bool causal, str pv=\"\") -> "
+  m.def("int8_fwd(Tensor q, Tensor k, Tensor v, bool smooth, bool causal) -> "
         "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("int8_bwd(Tensor dO, Tensor q_i8, Tensor sq, Tensor k_i8, Tensor sk, Tensor v_i8, Tensor sv, "
         "Tensor O, Tensor lse, bool causal, int kv_heads) -> (Tensor, Tensor, Tensor)");

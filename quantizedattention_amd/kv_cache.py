@@ -20,10 +20,9 @@ Wire format (little-endian, version 1)::
                                                             index (b * kv_heads + h) * tokens / 32 + s / 32
       k_mean  float16 [batch, kv_heads, 1, head_dim]        only when "smoothed" (SageAttention k-smoothing)
 
-The forward's P.V operand is not stored either: :meth:`QuantizedKV.operand` rebuilds it on the GPU
-from v_i8 (and sv) -- f16(v_i8 * sv) for the f16 P.V mode (``qattn_int8_dequant``), the int8 V^T
-operand image for the int8 mode (``qattn_int8_v_image``) -- bit-identically to the quantisers' own
-outputs.
+The forward's P.V operand is not stored either: :meth:`QuantizedKV.vt` rebuilds the int8 V^T
+operand image from v_i8 on the GPU (``qattn_int8_v_image``), bit-identically to the quantiser's own
+output; :meth:`QuantizedKV.vdq` gives the dequantised values f16(v_i8 * sv) (``qattn_int8_dequant``).
 
 Causal attention against a cache aligns the LAST query with the LAST key (query i of the Sq new
 ones sits at position Sk - Sq + i and keeps the keys up to it: ``causal = 2`` of
@@ -69,7 +68,7 @@ class QuantizedKV:
         return tuple(self.k_i8.shape)
 
     def vdq(self) -> torch.Tensor:
-        """f16(v_i8 * sv) [B*Hkv*S, D], the f16-mode P.V operand (rebuilt on demand, cached)."""
+        """f16(v_i8 * sv) [B*Hkv*S, D], the dequantised values (rebuilt on demand, cached)."""
         if self._vdq is None:
             B, H, S, D = self.shape
             _lib.require_gpu(self.v_i8, self.sv)
@@ -80,7 +79,7 @@ class QuantizedKV:
         return self._vdq
 
     def vt(self) -> torch.Tensor:
-        """The int8 V^T operand image of v_i8 [B*Hkv*S, D] bytes, the int8-mode P.V operand."""
+        """The int8 V^T operand image of v_i8 [B*Hkv*S, D] bytes, the forward's P.V operand."""
         if self._vt is None:
             B, H, S, D = self.shape
             _lib.require_gpu(self.v_i8)
@@ -90,10 +89,6 @@ class QuantizedKV:
                       _lib.stream_of(self.v_i8))
             self._vt = out
         return self._vt
-
-    def operand(self, pv: str) -> torch.Tensor:
-        """The P.V operand of mode ``pv`` ("f16": f16(v_i8 * sv); "i8": the int8 V^T image)."""
-        return self.vdq() if _pv_mode(pv) == "f16" else self.vt()
 
     def drop_operands(self) -> None:
         """Free the cached P.V operand images (rebuilt on the next use); the cache proper is k_i8,
@@ -206,34 +201,23 @@ def quantize_kv(k: torch.Tensor, v: torch.Tensor, smooth: bool = True,
     km = None if k_mean is None else k_mean.to(torch.float16).contiguous()
     _lib.call("qattn_int8_quant", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(km), N, S, D,
               st)
-    # v: indices, scales and the P.V operand image of the default (int8) mode in one pass, 1 B per
-    # element; the f16 image (2 B per element) is built only if the f16 mode asks for it
+    # v: indices, scales and the P.V operand image in one pass, 1 B per element
     vt = torch.empty((N, D), dtype=torch.int8, device=dev)
     _lib.call("qattn_int8_quant_vt", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vt), N, D, st)
     return QuantizedKV(k_i8, v_i8, sk, sv, km, None, vt)
 
 
-def _pv_mode(pv):
-    from . import attention_int8
-    pv = attention_int8.PV_MODE if pv is None else pv
-    if pv not in attention_int8.PV_MODES:
-        raise _lib.QAttnError(f"qattn kv cache: unknown P.V mode {pv!r} (one of {attention_int8.PV_MODES})")
-    return pv
-
-
-def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False, pv=None):
+def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False):
     """int8 attention of fp16 queries [B, Hq, Sq, D] against a quantised cache (inference; no autograd).
 
     Hq must be a multiple of the cache's heads (grouped-query attention).  ``causal``: the Sq queries
     are the LAST Sq positions (query i keeps keys <= Sk - Sq + i), Sq <= Sk.  Returns (O fp16
     [B, Hq, Sq, D], lse fp16 [B*Hq*Sq]); without ``causal`` identical to the forward on the un-cached
-    tensors (bit-identical when one key split covers the cache).  ``pv``: the P.V mode (default
-    attention_int8.PV_MODE).
-    Non-causal with the int8 P.V at head_dim 128 runs in the decoding layout (_decode_split: the
+    tensors (bit-identical when one key split covers the cache).
+    Non-causal at head_dim 128 runs in the decoding layout (_decode_split: the
     grouped query heads of a key/value head in one workgroup, long caches split over the keys and
     merged); the results equal the one-pass forward's up to the merge's rounding (<= 2e-3).
     """
-    pv = _pv_mode(pv)
     B, Hkv, Sk, D = kv.shape
     if q.dim() != 4 or q.shape[0] != B or q.shape[3] != D or q.shape[1] % Hkv or q.shape[2] % BLOCK:
         raise _lib.QAttnError("qattn kv cache: q must be [B, G*Hkv, 32*n, D] for the cache's B, Hkv, D")
@@ -251,17 +235,12 @@ def attention_int8_cached(q: torch.Tensor, kv: QuantizedKV, causal: bool = False
     _lib.call("qattn_int8_quant", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), None, None, N, Sq, D, st)
     qks = float(torch.tensor(1.0 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
     mode = 2 if causal else 0          # bottom-right aligned causal mask
-    if not causal and pv != "f16" and D == 128:
+    if not causal and D == 128:
         _decode_split(q_i8, sq, kv, O, lse, B, Hq, Sq, qks, st)
         return O, lse
-    if pv == "f16":
-        _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
-                  _lib.ptr(kv.sk), _lib.ptr(kv.vdq()), _lib.ptr(O), _lib.ptr(lse), B * Hq, Sq, Sk,
-                  Hq // Hkv, mode, D, qks, st)
-    else:
-        _lib.call("qattn_int8_attn_fwd_i8pv_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
-                  _lib.ptr(kv.sk), _lib.ptr(kv.vt()), _lib.ptr(kv.sv), _lib.ptr(O), _lib.ptr(lse),
-                  B * Hq, Sq, Sk, Hq // Hkv, mode, D, qks, st)
+    _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
+              _lib.ptr(kv.sk), _lib.ptr(kv.vt()), _lib.ptr(kv.sv), _lib.ptr(O), _lib.ptr(lse),
+              B * Hq, Sq, Sk, Hq // Hkv, mode, D, qks, st)
     return O, lse
 
 
@@ -292,7 +271,7 @@ def _decode_split(q_i8, sq, kv, O, lse, B, Hq, Sq, qks, st):
         return
     ks = _split_plan(bhv, rows, Sk)
     if ks >= Sk:
-        _lib.call("qattn_int8_attn_fwd_i8pv_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
+        _lib.call("qattn_int8_attn_fwd_ex", _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(kv.k_i8),
                   _lib.ptr(kv.sk), _lib.ptr(kv.vt()), _lib.ptr(kv.sv), _lib.ptr(O), _lib.ptr(lse),
                   bhv, rows, Sk, 1, 0, D, qks, st)
         return

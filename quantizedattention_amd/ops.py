@@ -8,7 +8,7 @@ its fake (meta) implementation, for graph capture (``torch.compile``, ``torch.ex
 the autograd rules of ``int8_fwd`` and ``bf16_fwd`` (their backward operators).
 
     torch.ops.qattn.int8_quant(x, block) -> (idx, scale)
-    torch.ops.qattn.int8_fwd(q, k, v, smooth, causal, pv="") -> (O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
+    torch.ops.qattn.int8_fwd(q, k, v, smooth, causal) -> (O, lse, q_i8, k_i8, v_i8, sq, sk, sv)
     torch.ops.qattn.int8_bwd(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, causal, kv_heads)
         -> (dq, dk, dv)
     torch.ops.qattn.bf16_fwd(q, k, v, causal) -> (O, lse)
@@ -42,7 +42,7 @@ def _(x, block):
 
 
 @torch.library.register_fake("qattn::int8_fwd")
-def _(q, k, v, smooth, causal, pv=""):
+def _(q, k, v, smooth, causal):
     B, H, S, D = q.shape
     Nq, Nkv = B * H * S, k.shape[0] * k.shape[1] * k.shape[2]
     e = lambda *s, dt: q.new_empty(s, dtype=dt)  # noqa: E731
@@ -101,7 +101,7 @@ def _int8_backward_rule(ctx, dO, *_unused):
     # gradient of O only (the quantised outputs are not differentiable, int8:52-56); k smoothing
     # adds no gradient (softmax-invariant), so the same backward serves smooth and plain forwards
     O, lse, q_i8, k_i8, v_i8, sq, sk, sv = ctx.saved_tensors
-    rest = (None,) * (ctx.n_inputs - 3)   # smooth, causal, pv
+    rest = (None,) * (ctx.n_inputs - 3)   # smooth, causal
     if dO is None:
         return (None, None, None) + rest
     qd, kd, vd = ctx.dtypes
@@ -142,12 +142,10 @@ def int8_quant(x, block):
     return _ops.int8_quant(x, block)
 
 
-def int8_fwd(q, k, v, smooth, causal, pv=None):
-    """SageAttention-3 int8 forward (attention_int8.py:97-262, per (batch, head)).  ``pv``: the P.V
-    mode (attention_int8.PV_MODES), default attention_int8.PV_MODE -- the drop-ins' mode, so the
-    operator and ``sage_attention_3_int8`` run the same kernel."""
-    from . import attention_int8
-    return _ops.int8_fwd(q, k, v, smooth, causal, attention_int8.PV_MODE if pv is None else pv)
+def int8_fwd(q, k, v, smooth, causal):
+    """SageAttention-3 int8 forward (attention_int8.py:97-262, per (batch, head)); the same kernels
+    as ``sage_attention_3_int8``."""
+    return _ops.int8_fwd(q, k, v, smooth, causal)
 
 
 def int8_bwd(dO, q_i8, sq, k_i8, sk, v_i8, sv, O, lse, causal, kv_heads):

@@ -74,7 +74,7 @@ int main(int argc, char** argv) {
   CHECK_QA(qattn_int8_quant_img(q, q_i8, sq, nullptr, q_bf, nullptr, N, (int)S, D, st));
   CHECK_QA(qattn_int8_quant_img(k, k_i8, sk, nullptr, k_bf, k_mean, N, (int)S, D, st));
   CHECK_QA(qattn_int8_quant_vt(v, v_i8, sv, vt, N, D, st));
-  CHECK_QA(qattn_int8_attn_fwd_i8pv_ex(q_i8, sq, k_i8, sk, vt, sv, O, lse, B * H, S, S, 1, 0, D, qks, st));
+  CHECK_QA(qattn_int8_attn_fwd_ex(q_i8, sq, k_i8, sk, vt, sv, O, lse, B * H, S, S, 1, 0, D, qks, st));
   // backward (attention_int8._int8_backward: prologue, then the one-pass dS-record backward)
   void *dO_i8 = dalloc(i8b), *sdO = dalloc(sb), *LD = dalloc((size_t)N * 8), *dO_bf = dalloc(f16b);
   void *dq = dalloc(f16b), *dk = dalloc(f16b), *dv = dalloc(f16b);

@@ -32,16 +32,11 @@ def test_c_host_matches_the_python_drop_in(shape, tmp_path):
                        text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     q, k, v, dO = (ins[n].cuda() for n in ("q", "k", "v", "dO"))
-    # the Python drop-in: autograd function of attention_int8.py (P.V mode i8, as the C host)
+    # the Python drop-in: autograd function of attention_int8.py
     qq, kk, vv = (t.clone().requires_grad_(True) for t in (q, k, v))
-    old = A.PV_MODE
-    A.PV_MODE = "i8"
-    try:
-        out = A.sage_attention_3_int8(qq, kk, vv)
-        out.backward(dO)
-        O, lse, *_ = A._int8_forward(q, k, v, smooth=True, images=True, pv="i8")
-    finally:
-        A.PV_MODE = old
+    out = A.sage_attention_3_int8(qq, kk, vv)
+    out.backward(dO)
+    O, lse, *_ = A._int8_forward(q, k, v, smooth=True, images=True)
     torch.cuda.synchronize()
 
     def load(name, n):

@@ -67,7 +67,7 @@ def test_zero_and_constant_inputs(lib):
     vc = torch.full_like(v, 0.75)
     O2 = helion_atten_int8_hl_dot_fwd(k, k, vc)[0].float().cpu()
     O2_ref = R.int8_fwd(k.cpu(), k.cpu(), vc.cpu())[0].float()
-    assert (O2 - O2_ref).abs().max().item() <= 3e-2
+    assert (O2 - O2_ref).abs().max().item() <= 1e-2
     assert (O2 - 0.75).abs().max().item() <= (O2_ref - 0.75).abs().max().item() + 1e-2
     assert (O2 <= 0.75 + 1e-3).all()   # truncation only ever lowers P_i8
 
@@ -103,15 +103,13 @@ def test_decode_single_block_cache(lib):
     assert torch.equal(O, ref[0]) and torch.equal(lse, ref[1])
 
 
-@pytest.mark.parametrize("D,causal,pv", [(128, False, "i8"), (64, False, "i8"), (128, True, "i8"),
-                                         (128, False, "f16"), (64, False, "f16"), (128, True, "f16")])
-def test_running_max_moves_vs_oracle(lib, monkeypatch, D, causal, pv):
+@pytest.mark.parametrize("D,causal", [(128, False), (64, False), (128, True), (64, True)])
+def test_running_max_moves_vs_oracle(lib, D, causal):
     """Keys whose scale grows along the sequence (and q = k, a peaked diagonal): the row max climbs
     by far more than the deferred-max threshold (8 in log2 units) from tile to tile, so the rare
     rescale branch runs on most tiles, including while the previous tile's P.V is in flight."""
     from oracle import restate as R
     from quantizedattention_amd import attention_int8 as A
-    monkeypatch.setattr(A, "PV_MODE", pv, raising=False)
     g = torch.Generator().manual_seed(44)
     S = 256
     ramp = (1.0 + torch.arange(S, dtype=torch.float32) / 24.0).view(1, 1, S, 1)
@@ -126,25 +124,24 @@ def test_running_max_moves_vs_oracle(lib, monkeypatch, D, causal, pv):
         d_ref = (out[0].float().cpu() - ref[0].float()).abs().max().item()
         e_ours = (out[0].float().cpu() - exact).abs().max().item()
         e_ref = (ref[0].float() - exact).abs().max().item()
-        print(f"D={D} causal={causal} pv={pv}: |O-O_ref| {d_ref:.4f}  |O-exact| {e_ours:.4f}  "
+        print(f"D={D} causal={causal}: |O-O_ref| {d_ref:.4f}  |O-exact| {e_ours:.4f}  "
               f"|O_ref-exact| {e_ref:.4f}")
         lse_x = _exact_lse2(q, k, causal)
         dl_ref = (out[1].float().cpu() - ref[1].float()).abs().max().item()
         el_ours = (out[1].float().cpu().reshape(-1) - lse_x).abs().max().item()
         el_ref = (ref[1].float().reshape(-1) - lse_x).abs().max().item()
         print(f"   lse: |l-l_ref| {dl_ref:.4f}  |l-exact| {el_ours:.4f}  |l_ref-exact| {el_ref:.4f}")
-        # lse = f16(m + f16(log2 l)) on a stale (deferred) m and a larger l: up to 4 f16 steps at
-        # these magnitudes (|lse| 30 .. 64: 1 step = 2^-5), never further from exact than the reference
+        # lse = f16(m + f16(log2 l)) (int8:252): within 2 fp16 steps of the oracle's, and never
+        # further from exact than the oracle's
         ulp = 2.0 ** (math.floor(math.log2(max(1.0, ref[1].float().abs().max().item()))) - 10)
-        assert dl_ref <= max(1e-2, 4 * ulp)
-        assert el_ours <= el_ref + 4 * ulp
+        lerr = (out[1].float().cpu() - ref[1].float()).abs()
+        assert (lerr <= 2 * 2.0 ** -10 * ref[1].float().abs() + 1e-3).all(), dl_ref
+        assert el_ours <= el_ref + 2 * ulp
         # Peaked rows (a handful of keys carry the row sum): a single P_i8 step weighs ~1/127 of the
-        # row, and P_i8 = trunc(127 exp2(f16(S - tile max))) here vs the reference's
-        # trunc(exp2(f16(S - running max)) / sp) differ by one step now and then (f16 rounding of
-        # the log-domain differences).  Bar for these inputs: 3e-2 from the
-        # reference, and no further from exact attention than the reference is (+1e-2) -- measured
-        # 1.3e-2 .. 1.8e-2 from the reference with both 0.03 .. 0.89 from exact attention.
-        assert d_ref <= 3e-2
+        # row.  The tiles that can weigh that much take the reference's literal P chain (the vote of
+        # csrc/int8_attn_fwd.hip), so O stays within the north star's 1e-2 of the
+        # oracle here too (round 4, without the vote: 1.3e-2 .. 1.8e-2).
+        assert d_ref <= 1e-2
         assert e_ours <= e_ref + 1e-2
 
 
@@ -228,3 +225,21 @@ def test_mxfp4_running_max_moves_vs_oracle(lib):
         assert torch.equal(a.cpu().reshape(b.shape), b)
     assert (O.float().cpu() - RO.float()).abs().max().item() <= 2e-2
     assert (lse.cpu() - Rl).abs().max().item() <= 1e-4 * max(1.0, Rl.abs().max().item())
+
+
+def test_workspace_refusal_is_remembered(lib, monkeypatch):
+    """A backward workspace the allocator refuses is not requested again (each refusal flushes the
+    caching allocator) until the device has room for it; smaller ones still are."""
+    from quantizedattention_amd import _lib
+    dev = torch.device("cuda", torch.cuda.current_device())
+    _lib._WS_REFUSED.pop(dev.index, None)
+    huge = 1 << 46                     # 64 TiB: refused by any allocator
+    assert _lib.try_workspace(huge, dev) is None
+    assert _lib._WS_REFUSED[dev.index] == huge
+    calls = []
+    orig = torch.empty
+    monkeypatch.setattr(torch, "empty", lambda *a, **kw: calls.append(a) or orig(*a, **kw))
+    assert _lib.try_workspace(huge, dev) is None and not calls      # not asked again
+    ws = _lib.try_workspace(1 << 20, dev)                            # a smaller one is
+    assert ws is not None and ws.numel() == 1 << 20 and len(calls) == 1
+    _lib._WS_REFUSED.pop(dev.index, None)

@@ -4,11 +4,10 @@ Sq != Sk, head_dim 64 / 128, causal or not, partial workgroups), random per-tens
 max that keeps moving).  The moving-max case found a real defect; this widens the
 net.
 
-Bars: quantisation bit-exact; O no further from exact fp32 attention than the oracle
-is (+1e-2 |v|) and within 3e-2 |v| of it (1e-2 on random rows, peaked rows can move one P_i8 step);
-lse within 4 fp16 steps; grads relL2 <= 0.05 vs the oracle; the cached (decoding) forward within
+Bars: quantisation bit-exact; O within the north star's 1e-2 of the oracle (scaled by
+|v| / 4 where |v| > 4) and no further from exact fp32 attention than the oracle is (+1e-2, scaled);
+lse within 2 fp16 steps; grads relL2 <= 0.05 vs the oracle; the cached (decoding) forward within
 2e-3 |v| of the forward."""
-import math
 
 import pytest
 import torch
@@ -61,15 +60,15 @@ def test_int8_fuzz(lib, i):
     O = out[0].float().cpu()
     d_ref = (O - ref[0].float()).abs().max().item()
     assert torch.isfinite(O).all()
-    assert d_ref <= 3e-2 * vs, d_ref
+    assert d_ref <= 1e-2 * vs, d_ref
     if not causal:
         ex = _exact(q, k, v)
         e_ours = (O - ex).abs().max().item()
         e_ref = (ref[0].float() - ex).abs().max().item()
         assert e_ours <= e_ref + 1e-2 * vs, (e_ours, e_ref)
     lr = ref[1].float()
-    ulp = 2.0 ** (math.floor(math.log2(max(1.0, lr.abs().max().item()))) - 10)
-    assert (out[1].float().cpu() - lr).abs().max().item() <= max(1e-2, 4 * ulp)
+    lerr = (out[1].float().cpu() - lr).abs()
+    assert (lerr <= 2 * 2.0 ** -10 * lr.abs() + 1e-3).all(), lerr.max().item()
     # backward through the reference's bwd entry, against the oracle's
     dO = torch.randn((B, Hq, Sq, D), generator=torch.Generator().manual_seed(2000 + i)).half()
     O_, lse_, qi, kiT, vi, sq, sk, sv, Bq, Bkv = out

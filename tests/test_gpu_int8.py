@@ -20,17 +20,8 @@ def _inputs(shape, seed=0, scale=1.0):
     return [(torch.randn(shape, generator=g) * scale) for _ in range(3)]
 
 
-@pytest.fixture(params=["f16", "i8"])
-def pv(request, monkeypatch):
-    """Both P.V modes of the forward (f16 operands with the tile scale folded in / int8 MFMA with a
-    per-tile dequantisation): same P_i8 and scales, same tolerance."""
-    from quantizedattention_amd import attention_int8
-    monkeypatch.setattr(attention_int8, "PV_MODE", request.param)
-    return request.param
-
-
 @pytest.mark.parametrize("shape", SHAPES)
-def test_int8_fwd_matches_oracle(lib, shape, pv):
+def test_int8_fwd_matches_oracle(lib, shape):
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
     q, k, v = _inputs(shape)
     qh, kh, vh = q.half(), k.half(), v.half()
@@ -65,7 +56,7 @@ def test_int8_quant_edge_cases(lib):
     assert torch.equal(out[5].cpu(), ref[5])
 
 
-def test_int8_fwd_deterministic(lib, pv):
+def test_int8_fwd_deterministic(lib):
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
     q, k, v = [t.half().cuda() for t in _inputs((1, 4, 256, 128), seed=3)]
     a = helion_atten_int8_hl_dot_fwd(q, k, v)
@@ -73,7 +64,7 @@ def test_int8_fwd_deterministic(lib, pv):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
-def test_int8_fwd_large_size_properties(lib, pv):
+def test_int8_fwd_large_size_properties(lib):
     """North-star size (4,32,4096,128): finite; constant V reproduces the constant; one head
     checked against the oracle at full length."""
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
@@ -197,3 +188,74 @@ def test_sage_function_new_style(lib):
     assert torch.equal(gq, qd.grad) and torch.equal(gk, kd.grad) and torch.equal(gv, vd.grad)
     from quantizedattention_amd import attention_int8
     assert not attention_int8._IMAGES, "image hand-off entries leaked"
+
+
+@pytest.mark.parametrize("shape,causal,G", [((1, 2, 256, 128), False, 1), ((2, 4, 160, 64), True, 2),
+                                            ((1, 8, 96, 128), False, 4), ((1, 2, 384, 64), False, 1)])
+def test_int8_fwd_q_fused_bit_identical(lib, shape, causal, G):
+    """qattn_int8_attn_fwd_qf (q quantised in the attention kernel's prologue) equals the separate
+    quantiser + qattn_int8_attn_fwd_ex bit for bit: q_i8, sq, the bf16 image, O and lse."""
+    from quantizedattention_amd import _lib
+    B, H, S, D = shape
+    g = torch.Generator().manual_seed(21)
+    q = (torch.randn(shape, generator=g) * 3).half().cuda()
+    q[0, 0, :32] = 0                                   # an all-zero block (sq = 0)
+    k, v = ((torch.randn((B, H // G, S, D), generator=g) * 2).half().cuda() for _ in range(2))
+    N, Nkv = B * H * S, B * (H // G) * S
+    e = lambda *s_, dt: torch.empty(s_, dtype=dt, device="cuda")  # noqa: E731
+    ki, vi, vt = e(Nkv, D, dt=torch.int8), e(Nkv, D, dt=torch.int8), e(Nkv, D, dt=torch.int8)
+    sk, sv = e(Nkv // 32, dt=torch.float16), e(Nkv // 32, dt=torch.float16)
+    st = _lib.stream_of(q)
+    P = _lib.ptr
+    _lib.call("qattn_int8_quant", P(k), P(ki), P(sk), None, None, Nkv, S, D, st)
+    _lib.call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), Nkv, D, st)
+    qks = float(torch.tensor(1 / D ** 0.5 * 1.44269504, dtype=torch.float32))
+    outs = []
+    for fused in (False, True):
+        qi, sq = e(N, D, dt=torch.int8), e(N // 32, dt=torch.float16)
+        qb = e(N, D, dt=torch.bfloat16)
+        O, lse = e(N, D, dt=torch.float16), e(N, dt=torch.float16)
+        if fused:
+            _lib.call("qattn_int8_attn_fwd_qf", P(q), P(qi), P(sq), P(qb), P(ki), P(sk), P(vt), P(sv), P(O),
+                      P(lse), B * H, S, S, G, int(causal), D, qks, st)
+        else:
+            _lib.call("qattn_int8_quant_img", P(q), P(qi), P(sq), None, P(qb), None, N, S, D, st)
+            _lib.call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv), P(O), P(lse),
+                      B * H, S, S, G, int(causal), D, qks, st)
+        outs.append((qi, sq, qb, O, lse))
+    torch.cuda.synchronize()
+    for a, b_ in zip(*outs):
+        assert torch.equal(a.view(torch.uint8) if a.dtype == torch.int8 else a.view(torch.int16),
+                           b_.view(torch.uint8) if b_.dtype == torch.int8 else b_.view(torch.int16))
+
+
+@pytest.mark.parametrize("D,smooth,img", [(128, True, True), (64, False, False), (128, False, True)])
+def test_int8_quant_kv_bit_identical(lib, D, smooth, img):
+    """qattn_int8_quant_kv (k and v in one launch) equals qattn_int8_quant_img on k and
+    qattn_int8_quant_vt on v bit for bit."""
+    from quantizedattention_amd import _lib
+    B, H, S = 2, 3, 224
+    g = torch.Generator().manual_seed(22)
+    k, v = ((torch.randn((B, H, S, D), generator=g) * 4).half().cuda() for _ in range(2))
+    v[0, 1, 64:96] = 0
+    N = B * H * S
+    e = lambda *s_, dt: torch.zeros(s_, dtype=dt, device="cuda")  # noqa: E731
+    st, P = _lib.stream_of(k), _lib.ptr
+    km = e(B * H, D, dt=torch.float16) if smooth else None
+    if smooth:
+        _lib.call("qattn_kmean", P(k), P(km), B * H, S, D, st)
+    res = []
+    for fused in (False, True):
+        ki, vi, vt = e(N, D, dt=torch.int8), e(N, D, dt=torch.int8), e(N, D, dt=torch.int8)
+        sk, sv = e(N // 32, dt=torch.float16), e(N // 32, dt=torch.float16)
+        kb = e(N, D, dt=torch.bfloat16) if img else None
+        if fused:
+            _lib.call("qattn_int8_quant_kv", P(k), P(ki), P(sk), P(kb), P(km), P(v), P(vi), P(sv), P(vt),
+                      N, S, D, st)
+        else:
+            _lib.call("qattn_int8_quant_img", P(k), P(ki), P(sk), None, P(kb), P(km), N, S, D, st)
+            _lib.call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
+        res.append([t for t in (ki, sk, kb, vi, sv, vt) if t is not None])
+    torch.cuda.synchronize()
+    for a, b_ in zip(*res):
+        assert torch.equal(a, b_)

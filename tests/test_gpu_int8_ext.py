@@ -20,13 +20,6 @@ SHAPES = [(1, 4, 2, 128, 96, 64), (2, 4, 1, 64, 160, 128), (1, 2, 2, 160, 128, 1
           (1, 2, 2, 128, 128, 64)]
 
 
-@pytest.fixture(params=["f16", "i8"])
-def pv(request, monkeypatch):
-    from quantizedattention_amd import attention_int8
-    monkeypatch.setattr(attention_int8, "PV_MODE", request.param)
-    return request.param
-
-
 def _inputs(shape, seed=0):
     B, Hq, Hkv, Sq, Sk, D = shape
     g = torch.Generator().manual_seed(seed)
@@ -42,7 +35,7 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("shape", SHAPES + [(1, 8, 8, 256, 256, 128), (1, 4, 2, 96, 224, 64)])
 @pytest.mark.parametrize("causal", [False, True])
-def test_int8_fwd_gqa_causal(lib, shape, causal, pv):
+def test_int8_fwd_gqa_causal(lib, shape, causal):
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
     q, k, v = _inputs(shape, seed=1)
     ref = R.int8_fwd(q, k, v, causal=causal)
@@ -58,7 +51,7 @@ def test_int8_fwd_gqa_causal(lib, shape, causal, pv):
     assert (lerr <= 2 * 2.0 ** -10 * ref[1].float().abs() + 1e-3).all(), lerr.max().item()
 
 
-def test_int8_causal_first_row_is_first_value(lib, pv):
+def test_int8_causal_first_row_is_first_value(lib):
     """Causal row 0 keeps key 0 only: O[0] is the dequantised v[0] = v_i8[0] * sv (P_i8 = 127,
     sp = 1/127), up to the fp16 roundings of the two P.V operands."""
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd

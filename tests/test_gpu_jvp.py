@@ -183,3 +183,18 @@ def test_jvp_non_contiguous_inputs(lib, dtype):
     torch.cuda.synchronize()
     assert torch.equal(O, Oc) and torch.equal(tO, tOc) and torch.equal(lse, lsec)
     assert torch.equal(Op, Oc) and torch.equal(lsep, lsec)
+
+
+def test_jvp_deferred_forward_without_jvp_rule(lib, monkeypatch):
+    """A call that defers its O to the jvp rule (attention_jvp saw a tangent coming) but whose jvp
+    rule never runs gets O from the primal kernel, and leaves no deferred entry behind."""
+    from quantizedattention_amd import attention_jvp as J
+    g = torch.Generator(device="cuda").manual_seed(11)
+    q, k, v = (torch.randn((1, 2, 128, 64), device="cuda", generator=g).bfloat16() for _ in range(3))
+    plain = J.attention_jvp(q, k, v)          # no transform: the primal kernel
+    monkeypatch.setattr(J, "_jvp_follows", lambda tensors: True)
+    deferred = J.attention_jvp(q, k, v)       # deferred, and no jvp rule follows
+    torch.cuda.synchronize()
+    assert torch.equal(deferred, plain)
+    assert not getattr(J._DEFER, "pending", [])
+    assert not getattr(J._DEFER, "on", False)

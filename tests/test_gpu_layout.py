@@ -95,3 +95,35 @@ def test_quant_div_exhaustive(lib):
     b = bad.cpu().tolist()
     assert b[0] == 0, (f"{b[0]} mismatches; first: s=0x{b[1]:04x} x=0x{b[2]:04x} ref={b[3]} "
                        f"byte={b[4]} image=0x{b[5] & 0xffffffff:08x}")
+
+
+def test_exp2_cr_on_f16_domain(lib):
+    """v_exp_f32 plus the correction table csrc/exp2_corr.h (the literal P chain's exp2_cr) is the
+    correctly rounded exp2 on every fp16 argument in [-32, 0]; v_exp_f16 is correctly rounded on every
+    finite fp16 argument.  (The oracle's exp2 is the correctly rounded one, oracle/restate.py _exp2.)"""
+    import re
+    from pathlib import Path
+    import numpy as np
+    from quantizedattention_amd import _lib
+    e32 = torch.empty(65536, dtype=torch.int32, device="cuda")
+    e16 = torch.empty(65536, dtype=torch.int16, device="cuda")
+    _lib.call("qattn_probe_exp2_dom", _lib.ptr(e32), _lib.ptr(e16), _lib.stream_of(e32))
+    torch.cuda.synchronize()
+    g32 = e32.cpu().numpy().view(np.uint32).astype(np.int64)
+    g16 = e16.cpu().numpy().view(np.float16)
+    hdr = (Path(__file__).resolve().parents[1] / "quantizedattention_amd" / "csrc" / "exp2_corr.h").read_text()
+    body = hdr[hdr.index("g_exp2_corr[EXP2_CORR_WORDS] = {"):]
+    words = np.array([int(w, 16) for w in re.findall(r"0x([0-9a-f]{8})u", body)], dtype=np.uint64)
+    n = 0x5001
+    i = np.arange(n)
+    codes = (words[i // 16] >> (2 * (i % 16)).astype(np.uint64)) & 3
+    hb = (0x8000 | i).astype(np.uint16)
+    x = hb.view(np.float16).astype(np.float64)
+    cr = np.exp2(x).astype(np.float32).view(np.uint32).astype(np.int64)
+    fixed = g32[hb.astype(np.int64)] + (codes == 1) - (codes == 2)
+    assert np.array_equal(fixed, cr), int((fixed != cr).sum())
+    h = np.arange(65536, dtype=np.uint32).astype(np.uint16).view(np.float16)
+    fin = np.isfinite(h)
+    with np.errstate(over="ignore"):
+        cr16 = np.exp2(h.astype(np.float64)).astype(np.float16)
+    assert np.array_equal(g16[fin].view(np.uint16), cr16[fin].view(np.uint16))

@@ -196,11 +196,10 @@ def test_checker_flags_a_close_overwrite():
     assert _store_data_overwrites(old)[1] and not _store_data_overwrites(new)[1]
 
 
-# Kernels whose spills are known and accepted, none on a default path: the 3-wave (168-VGPR) f16
-# P.V forward (an alternative P.V mode) reloads a few dwords; the recomputing fused dK+dV kernels (the
-# fallback when no dS workspace fits) spill one dword, stored before and reloaded after their loops.
-SPILL_OK = ("int8_attn_fwd_kernelILi128ELi0ELb0E", "int8_bwd_kernelILi128ELi3ELb1ELb0E",
-            "int8_bwd_kernelILi128ELi3ELb0ELb0E")
+# Kernels whose spills are known and accepted, none on a default path: the recomputing fused dK+dV
+# kernels (the fallback when no dS workspace fits) spill one dword, stored before and reloaded after
+# their loops.
+SPILL_OK = ("int8_bwd_kernelILi128ELi3ELb1ELb0E", "int8_bwd_kernelILi128ELi3ELb0ELb0E")
 
 
 def test_no_register_spills(asm):

@@ -43,16 +43,9 @@ def _fp16(shape, seed):
     return torch.randn(shape, generator=torch.Generator().manual_seed(seed)).half()
 
 
-@pytest.fixture(params=["f16", "i8"])
-def pv(request, monkeypatch):
-    from quantizedattention_amd import attention_int8
-    monkeypatch.setattr(attention_int8, "PV_MODE", request.param)
-    return request.param
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("hq,hkv", [(4, 4), (4, 2), (8, 1)])
-def test_cached_attention_matches_forward(lib, hq, hkv, pv):
+def test_cached_attention_matches_forward(lib, hq, hkv):
     """Non-causal: the cached forward through the wire format is bit-identical to the forward on the
     un-cached tensors (same quantiser, same kernel)."""
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
@@ -72,7 +65,7 @@ def test_cached_attention_matches_forward(lib, hq, hkv, pv):
 @pytest.mark.gpu
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("sq", [32, 64])
-def test_cached_decode_vs_oracle(lib, causal, sq, pv):
+def test_cached_decode_vs_oracle(lib, causal, sq):
     """SURVEY §8f N3 against the oracle: a cache grown by append (128 + 32 tokens), moved through
     to_bytes / from_bytes, attended by Sq new queries; causal aligns the last query with the last key
     (query i keeps keys <= Sk - Sq + i: the decode step sees the whole prefix).  O within the int8
@@ -130,7 +123,7 @@ def test_cache_append_and_vdq(lib):
 
 
 @pytest.mark.gpu
-def test_cache_from_forward_outputs(lib, pv):
+def test_cache_from_forward_outputs(lib):
     from quantizedattention_amd.attention_int8 import helion_atten_int8_hl_dot_fwd
     from quantizedattention_amd.kv_cache import attention_int8_cached
     q = _fp16((2, 2, 64, 64), 6).cuda()

@@ -1,4 +1,4 @@
-"""Time the int8 attention forward kernels (both P.V modes) of one library (A/B dev tool:
+"""Time the int8 attention forward kernel of one library (A/B dev tool:
 tools/ab_build.sh builds variants, tools/ab_run.sh runs this over them).
 
     QATTN_AB=_ab/libqattn_<variant>.so python tools/ab_time.py [B,H,S,D] [causal]
@@ -24,6 +24,12 @@ lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 
 
 def entry(name):
+    if name == "qattn_int8_attn_fwd_ex" and getattr(lib, "qattn_int8_attn_fwd_i8pv_ex", None) is not None:
+        name_sig, name = name, "qattn_int8_attn_fwd_i8pv_ex"   # a round-4 library (same arguments)
+        fn = getattr(lib, name)
+        fn.argtypes = SIGNATURES[name_sig]
+        fn.restype = ctypes.c_int
+        return fn
     fn = getattr(lib, name, None)
     if fn is not None:
         fn.argtypes = SIGNATURES[name]
@@ -46,21 +52,14 @@ P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 e = lambda *s, dt: torch.empty(s, dtype=dt, device="cuda")  # noqa: E731
 qi, ki, vi = (e(N, D, dt=torch.int8) for _ in range(3))
 sq, sk, sv = (e(N // 32, dt=torch.float16) for _ in range(3))
-vdq, vt = e(N, D, dt=torch.float16), e(N, D, dt=torch.int8)
+vt = e(N, D, dt=torch.int8)
 O, lse = e(N, D, dt=torch.float16), e(N, dt=torch.float16)
 call("qattn_int8_quant", P(q), P(qi), P(sq), None, None, N, S, D, st)
 call("qattn_int8_quant", P(k), P(ki), P(sk), None, None, N, S, D, st)
-call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
-if entry("qattn_int8_quant_vt") is not None:
-    call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
+call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
-fns = {}
-if entry("qattn_int8_attn_fwd_ex") is not None:
-    fns["f16"] = lambda: call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse),
-                              B * H, S, S, 1, int(causal), D, qks, st)
-if entry("qattn_int8_attn_fwd_i8pv_ex") is not None:
-    fns["i8"] = lambda: call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv),
-                             P(O), P(lse), B * H, S, S, 1, int(causal), D, qks, st)
+fns = {"i8": lambda: call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv),
+                         P(O), P(lse), B * H, S, S, 1, int(causal), D, qks, st)}
 only = os.environ.get("QATTN_AB_MODES")
 if only:
     fns = {k_: f_ for k_, f_ in fns.items() if k_ in only.split(",")}
@@ -93,3 +92,10 @@ for mode, f in fns.items():
     print(f"  max|O - O[{ref_o['m']}]| = {dO:.3g}, max|lse - lse[{ref_o['m']}]| = {dl:.3g}")
     print(f"{name} pv={mode}{' causal' if causal else ''}: {t * 1e3:.1f} us  {ops / t / 1e9:.0f} TOPS "
           f"({ops / t / 1e9 / 5033 * 100:.1f}% i8 peak)  O/lse {digest}", flush=True)
+    cnt = getattr(lib, "qattn_fwd_lit_count", None)
+    if cnt is not None:   # -DQA_FWD_LIT_COUNT=1 builds: literal tiles per wave-tile since load
+        import numpy as np
+        buf = np.zeros(2, dtype=np.uint64)
+        cnt.argtypes = [ctypes.c_void_p]
+        cnt(buf.ctypes.data)
+        print(f"  literal wave-tiles {int(buf[0])} of {int(buf[1])} ({100 * buf[0] / max(1, buf[1]):.2f} %)")

@@ -50,7 +50,7 @@ for Sk in (128, 256, 512, 1024, 2048, 4096):
     P = _lib.ptr
 
     def f(causal=0):
-        _lib.call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv), P(O), P(lse),
+        _lib.call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv), P(O), P(lse),
                   B * H, Sq, Sk, 1, causal, D, qks, st)
     t = time_it(f)
     rows.append((Sk // 32, t))

@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from quantizedattention_amd._lib import SIGNATURES
 torch.cuda.init()
 lib = ctypes.CDLL(os.environ["QATTN_AB"], mode=ctypes.RTLD_GLOBAL)
-fn = lib.qattn_int8_attn_fwd_i8pv_ex; fn.argtypes = SIGNATURES["qattn_int8_attn_fwd_i8pv_ex"]
+fn = lib.qattn_int8_attn_fwd_ex; fn.argtypes = SIGNATURES["qattn_int8_attn_fwd_ex"]
 B, H, S, D = 4, 32, 4096, 128
 N = B * H * S
 g = torch.Generator(device="cuda").manual_seed(0)

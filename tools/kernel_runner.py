@@ -56,7 +56,7 @@ for name in [n for _ in range(reps) for n in names]:
     if name == "int8_fwd":
         _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse), B * H, S, D, qks, st)
     elif name == "int8_fwd_i8":
-        _lib.call("qattn_int8_attn_fwd_i8pv_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv), P(O), P(lse),
+        _lib.call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv), P(O), P(lse),
                   B * H, S, S, 1, 0, D, qks, st)
     elif name == "int8_dkdv":
         _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD),
