@@ -146,14 +146,15 @@ def int8_kernel_times(q, k, v, dO, n):
                                              P(vi), P(sv), P(vt), N, S, D, st),
         "quant_vt_kernel(v)": lambda: _lib.call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D,
                                                 st),
-        # the default forward: P.V on the int8 MFMA (the reference's hl.dot(P_i8, v_i8))
-        "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki),
-                                                  P(sk), P(vt), P(sv), P(O), P(lse), B * H, S, S, 1, 0,
-                                                  D, qks, st),
-        # the forward the drop-ins run: q quantised inside the attention kernel
-        "int8_attn_fwd_kernel<q fused>": lambda: _lib.call("qattn_int8_attn_fwd_qf", P(q), P(qi), P(sq), P(qb),
-                                                           P(ki), P(sk), P(vt), P(sv), P(O), P(lse), B * H,
-                                                           S, S, 1, 0, D, qks, st),
+        # the forward the drop-ins run (q quantised in its prologue; P.V on the int8 MFMA, the
+        # reference's hl.dot(P_i8, v_i8)), with its fixup launch (int8_attn_fwd.hip DEFER0)
+        "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd_qf", P(q), P(qi), P(sq), None,
+                                                  P(ki), P(sk), P(vt), P(sv), P(O), P(lse), B * H, S,
+                                                  S, 1, 0, D, qks, st),
+        # the C-ABI form on a pre-quantised q (qattn_int8_attn_fwd_ex)
+        "int8_attn_fwd_kernel<q_i8 in>": lambda: _lib.call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki),
+                                                           P(sk), P(vt), P(sv), P(O), P(lse), B * H, S,
+                                                           S, 1, 0, D, qks, st),
         "int8_bwd_prep": lambda: _lib.call("qattn_int8_bwd_prep", P(dO), P(O), P(lse), P(dOi), P(sdO),
                                            P(LD), P(ob), B * H, S, D, st),
         "int8_bwd_dkdv_kernel<dK+dV>": lambda: _lib.call("qattn_int8_bwd_dkdv", P(dOi), P(sdO), P(qi),

@@ -172,7 +172,21 @@ QA_DEVICE LitOut literal_chain(const v16i& acc, int mx, float cq, float skt, flo
 // own 32-row block -- exactly the Q fragment it needs, one lane (row, half) per 64 values, bit-exact
 // with quant_block32_kernel -- and writes q_i8 and sq (the forward's outputs, int8:259-262) and, when
 // qbf is not null, the bf16 image of q_i8 the backward reads.  No separate q pass over HBM.
-template <int D, bool CAUSAL, bool SPLIT = false, bool QF = false>
+// Deferred votes (DEFER).  The vote asks whether a tile can weigh more than 1/LIT_K of its row; the
+// row sum it can compare with is the one so far, but what matters is the FINAL one, and on rows many
+// keys carry the tiles that vote -- the first ones, before the sum has grown -- end up weighing
+// little (config 3: ~1.5 % of the tiles vote, ~4 % of the kernel's time if they took the literal
+// chain).  So the forward takes the fast chain on every tile and only writes down each vote -- the
+// tile's weight er and the running max m at the time, in LDS (no register is free across the loop),
+// NV slots per wave -- and at the end takes the votes again against the final row sums, each
+// weight rescaled by exp2(m_then - m).  A wave for which one still holds (or whose slots overflowed)
+// marks its rows with FIX_LSE16 (lse; FIX_M32: m of the split state), and the fixup launch (FIX: the
+// same kernel, voting at the tile, the literal chain where a vote holds) recomputes exactly those
+// waves and overwrites their O and lse; its workgroups without a marked wave exit at once.
+constexpr unsigned short FIX_LSE16 = 0x7e5au;    // an fp16 NaN no result carries
+constexpr unsigned FIX_M32 = 0x7fc0e5a5u;        // an fp32 NaN no result carries
+
+template <int D, bool CAUSAL, bool SPLIT = false, bool QF = false, bool FIX = false>
 __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_kernel(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
     const _Float16* __restrict__ sk, const int8_t* __restrict__ vt, const _Float16* __restrict__ sv,
@@ -180,7 +194,9 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
     float qks, const _Float16* __restrict__ q16, __bf16* __restrict__ qbf) {
   static_assert(!SPLIT || !CAUSAL, "key splits: non-causal");
   static_assert(!SPLIT || !QF, "key splits: pre-quantised q");
+  static_assert(!FIX || !QF, "the fixup reads the q_i8 the forward wrote");
   using C = Int8FwdCfg<D>;
+  constexpr bool DEFER = C::LIT_K > 0 && QA_FWD_DEFER > 0 && !FIX;
   FWD_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per-tile scales: ck = sk * qks (f32), sv / 127 (f32)
@@ -196,9 +212,27 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   const int h = lane >> 5;
   const int c32 = lane & 31;
   const int q0 = qt * C::QROWS + wave * 32;
-  const bool active = q0 < Sq;
+  bool active = q0 < Sq;
   const long head_row0 = (long)bh * Sq;           // this head's query rows
   const int split = SPLIT ? (int)__builtin_amdgcn_readfirstlane(blockIdx.y) : 0;
+  if constexpr (FIX) {   // the waves the forward marked; a workgroup without one exits at once
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < C::WAVES; ++w) {
+      const int r0 = qt * C::QROWS + w * 32;
+      bool f = false;
+      if (r0 < Sq) {
+        if constexpr (SPLIT)
+          f = __float_as_uint(reinterpret_cast<const float2*>(lse)[((long)split * BH + bh) * Sq + r0].x) ==
+              FIX_M32;
+        else
+          f = __builtin_bit_cast(unsigned short, lse[head_row0 + r0]) == FIX_LSE16;
+      }
+      any = any || f;
+      if (w == wave) active = active && f;
+    }
+    if (!any) return;
+  }
   const int ks = qoff;                             // SPLIT (non-causal): keys per split
   const int k0 = SPLIT ? split * ks : 0;           // first key of this workgroup's key range
   const int nk = SPLIT ? min(ks, Sk - k0) : Sk;    // its keys
@@ -225,7 +259,8 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
     ck_lds[i] = (float)sk[kv_row0 / 32 + ti] * qks;
     svq_lds[i] = (float)sv[kv_row0 / 32 + ti] * (1.0f / 127.0f);
   }
-  for (int i = tid; i < EXP2_CORR_WORDS; i += 64 * C::WAVES) corr_lds[i] = g_exp2_corr[i];
+  if constexpr (!DEFER)   // (the forward with deferred votes never runs the literal chain)
+    for (int i = tid; i < EXP2_CORR_WORDS; i += 64 * C::WAVES) corr_lds[i] = g_exp2_corr[i];
   const float ck0 = (float)sk[kv_row0 / 32] * qks;   // tile 0 (the prologue's SM1)
   const float svq0 = (float)sv[kv_row0 / 32] * (1.0f / 127.0f);
 
@@ -299,6 +334,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   // the dequantisation factor of the tile whose P.V is in flight while SM1 of the next tile runs;
   // a running-max move there rescales it with O (its int32 product is added after SM1)
   float cpv_pend = 0.f;
+  int nvote = 0;            // (DEFER) votes written down so far (NV slots; more mark the wave)
 
   // ring slot u (the loop below passes compile-time slot numbers: LDS offsets become immediates)
   auto slot_at = [&](int u) -> const char* { return smem + u * C::SLOT; };
@@ -419,6 +455,9 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
     if constexpr (C::LIT_K > 0) lit = lit || __ballot(st.er * (0.5f * C::LIT_K) > l) != 0;
     if constexpr (C::LIT_K == 0) lit = true;
     lit = lit && live;
+#if defined(QA_FWD_LIT_LOOP) && QA_FWD_LIT_LOOP == 0   // (A/B: votes only in the prologue's tile 0)
+    lit = lit && (diag || !decltype(pend)::value);
+#endif
 #ifdef QA_FWD_LIT_NEVER   // (A/B: the vote and the chain's code, never taken)
     lit = lit && qks < 0.f;
 #endif
@@ -428,6 +467,16 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
       if (lit) atomicAdd(&g_fwd_lit[0], 1ull);
     }
 #endif
+    if (DEFER && lit) {   // write the vote down (a wave-uniform branch); the tile stays fast
+      if (nvote < C::NV) {
+        const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        unsigned* cs = corr_lds + EXP2_CORR_WORDS + (wave * C::NV + nvote) * 128 + ln;
+        cs[0] = __float_as_uint(st.er);
+        cs[64] = (unsigned)__builtin_bit_cast(unsigned short, m);
+      }
+      ++nvote;
+      lit = false;
+    }
     if (lit) {
       asm volatile("" ::: "memory");
       if constexpr (decltype(pend)::value) {
@@ -442,7 +491,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
       st.er = 0.f;
       st.cpv = r.cpv;
       mt = r.mt;
-    } else if (mx != INT_MIN && rm > mt) {
+    } else if (!DEFER && mx != INT_MIN && rm > mt) {   // (only the literal chain reads mt)
       mt = rm;
     }
   };
@@ -509,7 +558,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
     // groups of NSLOT = 4 tiles with compile-time ring slots (immediate LDS offsets, one 16-B read
     // of each scale table per group), then the remaining tiles with run-time slots
     static_assert(C::NSLOT == 4, "ring of 4 slots");
-    constexpr bool UNROLL = QA_FWD_UNROLL && !CAUSAL;
+    constexpr bool UNROLL = QA_FWD_UNROLL && !CAUSAL && (QF || FIX || SPLIT);
     const std::false_type nodiag{};
     int t = 0;
     for (; UNROLL && t + 4 <= tmain; t += 4) {
@@ -537,10 +586,31 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   FWD_STAMP(2);
 
   if (!active) return;
+  // (DEFER) the votes against the final row sums: mark the wave for the fixup
+  bool fix = false;
+  if (DEFER && nvote > 0) {
+    const float lrow = pair_sum(l) * (1.0f / (float)C::LIT_K);
+    if (nvote > C::NV) {
+      fix = true;
+    } else {
+      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      const unsigned* cs = corr_lds + EXP2_CORR_WORDS + wave * C::NV * 128 + ln;
+      bool any = false;
+#pragma unroll
+      for (int c = 0; c < C::NV; ++c) {
+        if (c >= nvote) break;
+        const float w = __uint_as_float(cs[128 * c]) *
+                        exp2_f32((float)__builtin_bit_cast(_Float16, (unsigned short)cs[128 * c + 64]) - (float)m);
+        any = any || w > lrow;
+      }
+      fix = __ballot(any) != 0;
+    }
+  }
   if constexpr (SPLIT) {   // the partial state of this key range: {m, l} and f16(O / l)
     l = pair_sum(l);
     const long prow = ((long)split * BH + bh) * Sq + q0;
-    if (h == 0) reinterpret_cast<float2*>(lse)[prow + c32] = float2{(float)m, l};
+    if (h == 0)
+      reinterpret_cast<float2*>(lse)[prow + c32] = float2{fix ? __uint_as_float(FIX_M32) : (float)m, l};
     const float inv = 1.0f / l;
     store_rows<D, _Float16, 1, true>(o, inv, smem + wave * RowTile<D, _Float16>::BYTES,
                                      out + prow * D, lane, -KMAG * obias * inv);
@@ -549,7 +619,9 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   // ---------------- epilogue: lse = fp16(m + fp16(log2 l)); O = fp16(O / l)   (int8:252-257)
   l = pair_sum(l);
   const long qrow = head_row0 + q0 + c32;
-  if (h == 0) lse[qrow] = (_Float16)((float)m + (float)(_Float16)log2_f32(l));
+  if (h == 0)
+    lse[qrow] = fix ? __builtin_bit_cast(_Float16, FIX_LSE16)
+                    : (_Float16)((float)m + (float)(_Float16)log2_f32(l));
   const float inv = 1.0f / l;
   store_rows<D, _Float16, 1, true>(o, inv, smem + wave * RowTile<D, _Float16>::BYTES,
                                    out + (head_row0 + q0) * D, lane, -KMAG * obias * inv);
@@ -573,6 +645,14 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
                      (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
                      (const int8_t*)vt, (const _Float16*)sv, (_Float16*)out, (_Float16*)lse, (int)bh,
                      (int)sq_tok, (int)sk_tok, group, qoff, qks, (const _Float16*)q16, (__bf16*)qbf);
+  if constexpr (C::LIT_K > 0 && QA_FWD_DEFER) {   // the waves whose first tile must be redone
+    auto fixk = int8_attn_fwd_kernel<D, CAUSAL, false, false, true>;
+    { static int granted_ = 0; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
+    hipLaunchKernelGGL(fixk, dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds, st,
+                       (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
+                       (const int8_t*)vt, (const _Float16*)sv, (_Float16*)out, (_Float16*)lse, (int)bh,
+                       (int)sq_tok, (int)sk_tok, group, qoff, qks, nullptr, nullptr);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -623,6 +703,14 @@ static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, 
                      (const int8_t*)k_i8, (const _Float16*)sk, (const int8_t*)vt, (const _Float16*)sv,
                      (_Float16*)opart, (_Float16*)ml, (int)bh, (int)sq_tok, (int)sk_tok, group, ks, qks,
                      nullptr, nullptr);
+  if constexpr (C::LIT_K > 0 && QA_FWD_DEFER) {   // the split rows whose first tile must be redone
+    auto fixk = int8_attn_fwd_kernel<D, false, true, false, true>;
+    { static int granted_ = 0; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
+    hipLaunchKernelGGL(fixk, dim3((unsigned)(nq * bh), (unsigned)nsplit), dim3(64 * C::WAVES), lds, st,
+                       (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
+                       (const int8_t*)vt, (const _Float16*)sv, (_Float16*)opart, (_Float16*)ml, (int)bh,
+                       (int)sq_tok, (int)sk_tok, group, ks, qks, nullptr, nullptr);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -688,7 +776,7 @@ extern "C" int qattn_int8_attn_fwd_qf(const void* q, void* q_i8, void* sq, void*
                                       const void* sk, const void* vt, const void* sv, void* out,
                                       void* lse, long bh, long sq_tok, long sk_tok, int group,
                                       int causal, int head_dim, float qks, void* stream) {
-  if (q == nullptr || q_i8 == nullptr || sq == nullptr) return 1;
+  if ((q == nullptr || q_i8 == nullptr || sq == nullptr) && bh != 0 && sq_tok != 0) return 1;
   return fwd_dispatch(q_i8, sq, k_i8, sk, vt, sv, out, lse, bh, sq_tok, sk_tok, group, causal,
                       head_dim, qks, q, q_bf, stream);
 }

@@ -26,6 +26,12 @@ namespace qattn {
 #ifndef QA_FWD_LIT_K
 #define QA_FWD_LIT_K 2
 #endif
+//   QA_FWD_DEFER    N > 0: the votes are taken again against the final row sums, N slots per wave
+//                   (every tile takes the fast chain; the waves whose vote still holds are recomputed
+//                   by a fixup launch that votes at the tile, int8_attn_fwd.hip); 0: vote at the tile.
+#ifndef QA_FWD_DEFER
+#define QA_FWD_DEFER 8
+#endif
 
 template <int D>
 struct Int8FwdCfg {
@@ -49,9 +55,11 @@ struct Int8FwdCfg {
   static constexpr int CORR_BYTES = EXP2_CORR_WORDS * 4;   // the exp2 correction table (LDS copy)
   static constexpr float THR = QA_FWD_THR;   // deferred running-max threshold (log2 units)
   static constexpr int LIT_K = QA_FWD_LIT_K;
+  static constexpr int NV = QA_FWD_DEFER > 0 ? QA_FWD_DEFER : 1;   // deferred-vote slots per wave
+  static constexpr int CAND_BYTES = WAVES * NV * 128 * 4;           // {er, m} per lane and slot
   // LDS bytes of a launch over nt key tiles: ring, two per-tile scale tables (padded to 4 tiles),
-  // the correction table
-  static constexpr int lds_bytes(int nt) { return RING + ((nt + 3) / 4 * 4) * 8 + CORR_BYTES; }
+  // the correction table, the deferred vote
+  static constexpr int lds_bytes(int nt) { return RING + ((nt + 3) / 4 * 4) * 8 + CORR_BYTES + CAND_BYTES; }
 };
 
 template <int D>

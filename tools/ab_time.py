@@ -60,6 +60,10 @@ call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
 fns = {"i8": lambda: call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv),
                          P(O), P(lse), B * H, S, S, 1, int(causal), D, qks, st)}
+if getattr(lib, "qattn_int8_attn_fwd_qf", None) is not None:   # q quantised in the kernel
+    qi2, sq2 = e(N, D, dt=torch.int8), e(N // 32, dt=torch.float16)
+    fns["qf"] = lambda: call("qattn_int8_attn_fwd_qf", P(q), P(qi2), P(sq2), None, P(ki), P(sk), P(vt),
+                             P(sv), P(O), P(lse), B * H, S, S, 1, int(causal), D, qks, st)
 only = os.environ.get("QATTN_AB_MODES")
 if only:
     fns = {k_: f_ for k_, f_ in fns.items() if k_ in only.split(",")}

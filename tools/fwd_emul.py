@@ -48,7 +48,7 @@ def kmag_scale(c):
     return b.view(F32).astype(np.float64)
 
 
-def emulate(qi, sq, ki, sk, vi, sv, qks, K=None, thr=8.0, lse_from_mt=False, wave=32):
+def emulate(qi, sq, ki, sk, vi, sv, qks, K=None, thr=8.0, lse_from_mt=False, wave=32, NC=0):
     """One head: qi [S,D], ki/vi [Sk,D] int8 (as int64 arrays), sq/sk/sv f16 per 32-row block.
     K: the vote bar (a tile takes the literal chain when some row of its wave has er*K > l);
     None = never (the current kernel), 0 = always.  Returns O (f16 as f64), lse, literal fraction."""
@@ -63,7 +63,10 @@ def emulate(qi, sq, ki, sk, vi, sv, qks, K=None, thr=8.0, lse_from_mt=False, wav
     lrow = np.zeros(S)
     O = np.zeros((S, D))
     nlit = 0
+    nredo = 0
     qks32 = float(np.float32(qks))
+    nw = S // wave
+    cands = [[] for _ in range(nw)]   # per wave: deferred candidates (tile, fast and literal parts)
     for t in range(nt):
         ks = slice(32 * t, 32 * t + 32)
         X = (qi @ ki[ks].T).astype(np.float64)                   # exact integer dot
@@ -81,6 +84,10 @@ def emulate(qi, sq, ki, sk, vi, sv, qks, K=None, thr=8.0, lse_from_mt=False, wav
         m_thr = np.where(mv, h(m + thr), m_thr)
         lrow *= r
         O *= r[:, None]
+        for w_ in range(nw):   # deferred candidates rescale with O
+            rs = slice(w_ * wave, (w_ + 1) * wave)
+            for cd in cands[w_]:
+                cd["scale"] *= r[rs]
         er = exp2_cr32(h(rm - m))
         if K is None:
             lit = np.zeros(S, bool)
@@ -88,6 +95,15 @@ def emulate(qi, sq, ki, sk, vi, sv, qks, K=None, thr=8.0, lse_from_mt=False, wav
             lit = np.ones(S, bool)
         else:
             lit = (er * K > lrow).reshape(-1, wave).any(1).repeat(wave)
+        # NC > 0: the first NC voting tiles of a wave go fast now and are redone at the end if the
+        # final row sum still says so (deferred vote); later ones go literal now
+        defer = np.zeros(S, bool)
+        if NC > 0 and K not in (None, 0):
+            for w_ in range(nw):
+                rs = slice(w_ * wave, (w_ + 1) * wave)
+                if lit[rs][0] and len(cands[w_]) < NC:
+                    defer[rs] = True
+            lit = lit & ~defer
         nlit += lit.reshape(-1, wave)[:, 0].sum()
         # fast chain
         d = h(S16 - rm[:, None])
@@ -96,6 +112,24 @@ def emulate(qi, sq, ki, sk, vi, sv, qks, K=None, thr=8.0, lse_from_mt=False, wav
         cpv = er * f(float(sv[t]) * f(1.0 / 127.0))
         lt = er * e.sum(1)
         # literal chain (the reference's, int8:197-237, exp2 correctly rounded)
+        if defer.any():
+            Sr = h(f(f(f(X * sqr[:, None]) * skt) * qks32))
+            rmr = Sr.max(1)
+            nmr = np.maximum(mt, rmr)
+            P = exp2_cr32(h(Sr - nmr[:, None]))
+            sp = f(exp2_cr32(h(rmr - nmr)) / 127.0)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                Pir = np.where(sp[:, None] > 0, np.trunc(f(P / np.where(sp > 0, sp, 1.0)[:, None])), 0.0)
+            wv = exp2_cr32(nmr - m)
+            Vt = vi[ks].astype(np.float64)
+            for w_ in range(nw):
+                rs = slice(w_ * wave, (w_ + 1) * wave)
+                if defer[rs][0]:
+                    cands[w_].append(dict(
+                        fastO=(Pi[rs] @ Vt) * cpv[rs, None], fastl=lt[rs], er=er[rs],
+                        litO=(Pir[rs] @ Vt) * (f(sp[rs] * float(sv[t])) * wv[rs])[:, None],
+                        litl=f(P[rs].sum(1)) * wv[rs], scale=np.ones(wave)))
+            mt = np.where(defer, nmr, mt)
         if lit.any():
             Sr = h(f(f(f(X * sqr[:, None]) * skt) * qks32))
             rmr = Sr.max(1)
@@ -115,6 +149,13 @@ def emulate(qi, sq, ki, sk, vi, sv, qks, K=None, thr=8.0, lse_from_mt=False, wav
             mt = np.maximum(mt, rm)
         lrow += lt
         O += (Pi @ vi[ks].astype(np.float64)) * cpv[:, None]
+    for w_ in range(nw):   # the deferred vote on the final row sums
+        rs = slice(w_ * wave, (w_ + 1) * wave)
+        for cd in cands[w_]:
+            if np.any(cd["er"] * cd["scale"] * K > lrow[rs]):
+                nredo += 1
+                O[rs] += (cd["litO"] - cd["fastO"]) * cd["scale"][:, None]
+                lrow[rs] += (cd["litl"] - cd["fastl"]) * cd["scale"]
     if lse_from_mt:
         lref = f(lrow * exp2_cr32(m - mt))
         lse = h(mt + h(np.log2(lref)))
