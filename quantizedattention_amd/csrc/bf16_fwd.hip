@@ -182,7 +182,16 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
     float r;
   };
   const float inf = INFINITY;
+  // causal: a 16-key sub-tile whose first key is at or past the wave's last query is masked for
+  // every row (S = -126 throughout, bf16:222-233): its S, top two and P need no per-score work
+  auto masked = [&](int t, int u) { return CAUSAL && t * C::KT + 16 * u >= q0 + 31; };
   auto phase_a = [&](Sub& x, int t, int u, const v16f& acc) {
+    if (masked(t, u)) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x.s[j] = -126.0f;
+      x.M1 = x.M2 = -126.0f;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       const unsigned hh = pk_f16(acc[8 * u + j], acc[8 * u + j + 1]);
@@ -212,7 +221,7 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
         __builtin_amdgcn_fmed3f(__builtin_amdgcn_fmed3f(a1, b1, -inf), __uint_as_float(x2[0]), inf),
         __uint_as_float(x2[1]), inf);
   };
-  auto phase_b = [&](Sub& x) {
+  auto phase_b = [&](Sub& x, bool msk) {
     float nm = __builtin_amdgcn_fmed3f(m, rne1(x.M1 * qks), inf);   // bf16:236-239
     const float thr = rne1(nm - thr_eps);                            // bf16:248
     // #{S >= thr} > 1  <=>  second largest >= thr:  m' = 2m' (m' > 0) | 0 (m' < 0)   bf16:248-264
@@ -220,12 +229,18 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
     nm = (x.M2 >= thr && nm != 0.f) ? dbl : nm;
     // P = bf16(exp2(bf16(bf16(S*qks) - nm))).  Scalar fp32 on purpose: v_pk_*_f32 issue through
     // the matrix pipe and stall ~38 cycles behind the co-resident wave's MFMAs (tools/ubench).
+    if (msk) {   // every S is -126: one P for the lane's 8 scores (the same operations)
+      const float p = exp2_f32(rne1(rne1(-126.0f * qks) - nm));
+      const unsigned w = pk_bf16(p, p);
+      x.pk = v4u{w, w, w, w};
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      float a, b;
-      rne2(x.s[j] * qks, x.s[j + 1] * qks, a, b);
-      rne2(a - nm, b - nm, a, b);
-      x.pk[j / 2] = pk_bf16(exp2_f32(a), exp2_f32(b));
+      for (int j = 0; j < 8; j += 2) {
+        float a, b;
+        rne2(x.s[j] * qks, x.s[j + 1] * qks, a, b);
+        rne2(a - nm, b - nm, a, b);
+        x.pk[j / 2] = pk_bf16(exp2_f32(a), exp2_f32(b));
+      }
     }
     x.r = rne1(exp2_f32(rne1(m - nm)));                              // bf16:276
     m = nm;
@@ -263,12 +278,14 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
     ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
     dma.issue(smem_lds + decltype(FRc)::value * C::SLOT, min(t + 3, nt - 1));
     {
-      const v16f nacc = qk(NXc);
+      // (a tile masked for the whole wave needs no S: its QK^T MFMAs are skipped)
+      v16f nacc = v16f{};
+      if (!masked(t + 1, 0)) nacc = qk(NXc);
       Sub x0, x1;
       phase_a(x0, t, 0, acc);
       phase_a(x1, t, 1, acc);
-      phase_b(x0);
-      phase_b(x1);
+      phase_b(x0, masked(t, 0));
+      phase_b(x1, masked(t, 1));
       phase_c(SLc, x0, 0);
       phase_c(SLc, x1, 1);
       acc = nacc;

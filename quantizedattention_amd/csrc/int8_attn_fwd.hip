@@ -88,6 +88,12 @@ struct SmTile {
 #ifndef QA_FWD_UNROLL
 #define QA_FWD_UNROLL 1
 #endif
+// Timing-only ablations of the ring skeleton (-DQA_FWD_ABL=N, tools/ab_time.py; wrong results):
+// 1 no wait+barrier on odd tiles of the unrolled group, 2 also one DMA issue (2 tiles) per 2 tiles,
+// 3 no DMA after the prologue, 4 no wait+barrier in the loop
+#ifndef QA_FWD_ABL
+#define QA_FWD_ABL 0
+#endif
 // Diagnostic build only (-DQA_FWD_LIT_COUNT=1, tools/ab_time.py): counts the literal wave-tiles and
 // all wave-tiles (vector atomics by lane 0 of each wave).
 #ifndef QA_FWD_LIT_COUNT
@@ -521,9 +527,22 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   // (its row max cannot move m, and its state is never used) and it keeps the loop body branch-free.
   //   cur, nxt: ring slots of tiles t and t+1; fill: the slot the DMA of tile t+3 goes to (freed by
   //   the barrier); ckn, svqn: the scales of tile t+1
-  auto iter = [&](int t, int cur, int nxt, int fill, float ckn, float svqn, auto dg) {
+  auto iter = [&](int t, int cur, int nxt, int fill, float ckn, float svqn, auto dg, auto pos) {
+#if QA_FWD_ABL   // (timing-only ablations of the ring skeleton: results are wrong)
+    constexpr int P = decltype(pos)::value;
+    if (QA_FWD_ABL == 4 || ((QA_FWD_ABL == 1 || QA_FWD_ABL == 2) && (P & 1))) {
+    } else {
+      ring_wait_barrier<C::IPW>();
+    }
+    if (QA_FWD_ABL == 3 || (QA_FWD_ABL == 2 && (P & 1))) {
+    } else {
+      dma.issue(smem_lds + fill * C::SLOT, min(t + 3, nt - 1));
+      if (QA_FWD_ABL == 2 && P >= 0) dma.issue(smem_lds + ((fill + 1) & 3) * C::SLOT, min(t + 4, nt - 1));
+    }
+#else
     ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot `fill` is free
     dma.issue(smem_lds + fill * C::SLOT, min(t + 3, nt - 1));
+#endif
     // Phase order (pinned: hipcc otherwise issues the QK(t+1) chain right before its consumer
     // SM1(t+1) and the wave stalls on it): fragment reads, the 16 exponentials of tile t (which
     // cover the LDS latency), QK(t+1), then the rest of SM2(t), PV(t) and SM1(t+1).
@@ -564,16 +583,17 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
     for (; UNROLL && t + 4 <= tmain; t += 4) {
       const v4f ck4 = *reinterpret_cast<const v4f*>(ck_lds + t);
       const v4f sv4 = *reinterpret_cast<const v4f*>(svq_lds + t);
-      iter(t, 0, 1, 3, ck4[0], sv4[0], nodiag);
-      iter(t + 1, 1, 2, 0, ck4[1], sv4[1], nodiag);
-      iter(t + 2, 2, 3, 1, ck4[2], sv4[2], nodiag);
-      iter(t + 3, 3, 0, 2, ck4[3], sv4[3], nodiag);
+      iter(t, 0, 1, 3, ck4[0], sv4[0], nodiag, std::integral_constant<int, 0>{});
+      iter(t + 1, 1, 2, 0, ck4[1], sv4[1], nodiag, std::integral_constant<int, 1>{});
+      iter(t + 2, 2, 3, 1, ck4[2], sv4[2], nodiag, std::integral_constant<int, 2>{});
+      iter(t + 3, 3, 0, 2, ck4[3], sv4[3], nodiag, std::integral_constant<int, 3>{});
     }
     for (; t < tmain; ++t)
-      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], nodiag);
+      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], nodiag, std::integral_constant<int, -2>{});
     if constexpr (CAUSAL) {
       for (; t < nt; ++t)
-        iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], std::true_type{});
+        iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], std::true_type{},
+             std::integral_constant<int, -2>{});
     }
   } else {   // a wave past the last query row: the barriers and the ring's DMA only
     for (int t = 0; t < nt; ++t) {
