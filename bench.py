@@ -142,10 +142,11 @@ def int8_kernel_times(q, k, v, dO, n):
                                                      P(kb), P(km), N, S, D, st),
         "quant_block32_kernel(q)": lambda: _lib.call("qattn_int8_quant_img", P(q), P(qi), P(sq), None,
                                                      P(qb), None, N, S, D, st),
-        "quant_kv_kernel": lambda: _lib.call("qattn_int8_quant_kv", P(k), P(ki), P(sk), P(kb), P(km), P(v),
-                                             P(vi), P(sv), P(vt), N, S, D, st),
         "quant_vt_kernel(v)": lambda: _lib.call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D,
                                                 st),
+        # the forward call's own quantiser launches (int8_fwd: no bf16 images)
+        "quant_block32_kernel(k, fwd)": lambda: _lib.call("qattn_int8_quant", P(k), P(ki), P(sk), None,
+                                                          P(km), N, S, D, st),
         # the forward the drop-ins run (q quantised in its prologue; P.V on the int8 MFMA, the
         # reference's hl.dot(P_i8, v_i8)), with its fixup launch (int8_attn_fwd.hip DEFER0)
         "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd_qf", P(q), P(qi), P(sq), None,

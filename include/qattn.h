@@ -59,12 +59,6 @@ int qattn_int8_dequant(const void* idx, const void* scale, void* deq, long rows,
  *   v_mfma_i32_32x32x32_i8 in the forward's key order).  rows % 32 == 0. */
 int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt, long rows, int head_dim,
                         void* stream);
-/* k and v of one forward in one launch: qattn_int8_quant_img on k (kmean / k_img optional, as
- * there) and qattn_int8_quant_vt on v, both [rows, D] with rows_per_head rows per head; the same
- * outputs bit for bit. */
-int qattn_int8_quant_kv(const void* k, void* k_i8, void* sk, void* k_img, const void* kmean,
-                        const void* v, void* v_i8, void* sv, void* vt, long rows, int rows_per_head,
-                        int head_dim, void* stream);
 /* vt of qattn_int8_quant_vt from stored indices v_i8 (a restored int8 key/value cache). */
 int qattn_int8_v_image(const void* v_i8, void* vt, long rows, int head_dim, void* stream);
 

@@ -26,7 +26,6 @@ SIGNATURES = {
     "qattn_int8_quant_img": [_vp] * 6 + [_c_long, _c_int, _c_int, _vp],
     "qattn_int8_dequant": [_vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_int8_quant_vt": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
-    "qattn_int8_quant_kv": [_vp] * 9 + [_c_long, _c_int, _c_int, _vp],
     "qattn_int8_v_image": [_vp, _vp, _c_long, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
     "qattn_int8_attn_fwd": [_vp] * 8 + [_c_long, _c_long, _c_int, _c_float, _vp],

@@ -96,10 +96,12 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
         k_mean = torch.empty((B, Hkv, 1, D), dtype=torch.float16, device=dev)
         _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(k_mean), B * Hkv, Sk, D, st)
     qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
-    # k (smoothed, with the backward's bf16 image when asked) and v (with its P.V operand image) in
-    # one launch
-    _lib.call("qattn_int8_quant_kv", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), _lib.ptr(k_bf),
-              _lib.ptr(k_mean), _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vt), Nkv, Sk, D, st)
+    # k (smoothed, with the backward's bf16 image when asked), then v with its P.V operand image
+    # (two launches: one launch alternating k and v workgroups measured 105 against 31 + 45 us at
+    # config 3)
+    _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
+              _lib.ptr(k_mean), Nkv, Sk, D, st)
+    _lib.call("qattn_int8_quant_vt", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vt), Nkv, D, st)
     # q is quantised inside the attention kernel (q_i8, sq and the bf16 image written there)
     _lib.call("qattn_int8_attn_fwd_qf", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(q_bf),
               _lib.ptr(k_i8), _lib.ptr(sk), _lib.ptr(vt), _lib.ptr(sv), _lib.ptr(O), _lib.ptr(lse),

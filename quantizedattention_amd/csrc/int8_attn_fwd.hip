@@ -527,9 +527,9 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   // (its row max cannot move m, and its state is never used) and it keeps the loop body branch-free.
   //   cur, nxt: ring slots of tiles t and t+1; fill: the slot the DMA of tile t+3 goes to (freed by
   //   the barrier); ckn, svqn: the scales of tile t+1
-  auto iter = [&](int t, int cur, int nxt, int fill, float ckn, float svqn, auto dg, auto pos) {
+  auto iter = [&](int t, int cur, int nxt, int fill, float ckn, float svqn, auto dg, int pos) {
 #if QA_FWD_ABL   // (timing-only ablations of the ring skeleton: results are wrong)
-    constexpr int P = decltype(pos)::value;
+    const int P = pos;   // (a constant at every call site: 0..3 in the unrolled group, -2 elsewhere)
     if (QA_FWD_ABL == 4 || ((QA_FWD_ABL == 1 || QA_FWD_ABL == 2) && (P & 1))) {
     } else {
       ring_wait_barrier<C::IPW>();
@@ -583,17 +583,17 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
     for (; UNROLL && t + 4 <= tmain; t += 4) {
       const v4f ck4 = *reinterpret_cast<const v4f*>(ck_lds + t);
       const v4f sv4 = *reinterpret_cast<const v4f*>(svq_lds + t);
-      iter(t, 0, 1, 3, ck4[0], sv4[0], nodiag, std::integral_constant<int, 0>{});
-      iter(t + 1, 1, 2, 0, ck4[1], sv4[1], nodiag, std::integral_constant<int, 1>{});
-      iter(t + 2, 2, 3, 1, ck4[2], sv4[2], nodiag, std::integral_constant<int, 2>{});
-      iter(t + 3, 3, 0, 2, ck4[3], sv4[3], nodiag, std::integral_constant<int, 3>{});
+      iter(t, 0, 1, 3, ck4[0], sv4[0], nodiag, 0);
+      iter(t + 1, 1, 2, 0, ck4[1], sv4[1], nodiag, 1);
+      iter(t + 2, 2, 3, 1, ck4[2], sv4[2], nodiag, 2);
+      iter(t + 3, 3, 0, 2, ck4[3], sv4[3], nodiag, 3);
     }
     for (; t < tmain; ++t)
-      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], nodiag, std::integral_constant<int, -2>{});
+      iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], nodiag, -2);
     if constexpr (CAUSAL) {
       for (; t < nt; ++t)
         iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], std::true_type{},
-             std::integral_constant<int, -2>{});
+             -2);
     }
   } else {   // a wave past the last query row: the barriers and the ring's DMA only
     for (int t = 0; t < nt; ++t) {

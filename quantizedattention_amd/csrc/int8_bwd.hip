@@ -241,9 +241,8 @@ struct BwdCfg {
 
 // LDS-DMA plan: per wave slot i the lane-constant source byte offset inside the region's tile, the
 // LDS offset inside the ring slot, the region's per-tile stride and its buffer descriptor.
-template <int D, int ROLE>
-struct BwdDma {
-  using G = BwdCfg<D, ROLE>;
+template <int D, typename G>
+struct BwdDmaT {
   unsigned voff[G::IPW16];
   unsigned lds_off[G::IPW16];
   unsigned stride[G::IPW16];
@@ -290,6 +289,8 @@ struct BwdDma {
     if constexpr (G::HAS_LD) dma4_buf(ld_rsrc, 4 * lane, (unsigned)t * 256, slot_lds + G::LDO);
   }
 };
+template <int D, int ROLE>
+using BwdDma = BwdDmaT<D, BwdCfg<D, ROLE>>;
 
 // Inline-asm VALU blocks here write only registers tied to their inputs ("+v"), as a precaution:
 // hipcc's hazard recogniser does not look inside inline asm, so an asm output placed in a register

@@ -15,6 +15,21 @@
 
 namespace qattn {
 
+// max |x| over 8 fp16 values folded into a running pair of u16 maxima: for finite halves the order of
+// |x| is the integer order of (bits & 0x7fff), so one v_and + one v_pk_max_u16 per pair (the f32 form
+// takes a conversion and a max per value).  amax_pk_f32 turns the pair into the float max.
+typedef unsigned short v2us __attribute__((ext_vector_type(2)));
+QA_DEVICE void amax_pk8(const v8h& x, v2us& acc) {
+  const v4u w = __builtin_bit_cast(v4u, x);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    acc = __builtin_elementwise_max(acc, __builtin_bit_cast(v2us, w[k] & 0x7fff7fffu));
+}
+QA_DEVICE float amax_pk_f32(v2us acc) {
+  const unsigned short m = acc[0] > acc[1] ? acc[0] : acc[1];
+  return (float)__builtin_bit_cast(_Float16, m);
+}
+
 // rows: total rows (multiple of 32); rows_per_head: S (for the k-mean lookup)
 // DEQ: also write f16(idx * s) (the forward's P.V operand for v); IMG: also write bf16(idx) (the
 // exact transposed-read image the backward's accumulating products use for q and k).
@@ -29,21 +44,28 @@ QA_DEVICE void quant_block32(const _Float16* __restrict__ x, int8_t* __restrict_
   v8h v[ITERS];
   const _Float16* km = nullptr;
   if constexpr (SMOOTH) km = kmean + (blk * 32 / rows_per_head) * D;
-  float amax = 0.f;
+  v2us am = {0, 0};
 #pragma unroll
   for (int i = 0; i < ITERS; ++i) {
     const int e = (i * 64 + lane) * 8;
     v[i] = *reinterpret_cast<const v8h*>(xb + e);
     if constexpr (SMOOTH) {
+      // f16(x - m) (eager fp16 `k - k_mean`): packed f16 subtraction, which rounds the exact
+      // difference once -- the same bits as rounding through fp32 first, since an fp32 difference
+      // of two fp16 values is inexact only when their exponents are more than 13 apart, and then
+      // both roundings return the larger operand
       const int d0 = e % D;
       const v8h m = *reinterpret_cast<const v8h*>(km + d0);
+      v2h xs[4], ms[4];
+      __builtin_memcpy(xs, &v[i], 16);
+      __builtin_memcpy(ms, &m, 16);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = (_Float16)((float)v[i][j] - (float)m[j]);
+      for (int k = 0; k < 4; ++k) xs[k] = xs[k] - ms[k];   // v_pk_add_f16 (neg)
+      __builtin_memcpy(&v[i], xs, 16);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf((float)v[i][j]));
+    amax_pk8(v[i], am);
   }
-  amax = wave_max_f(amax);
+  const float amax = wave_max_f(amax_pk_f32(am));
   const _Float16 s16 = (_Float16)(amax / 127.0f);
   const float s = (float)s16;
   const float r = quant_rcp(s);
@@ -94,16 +116,15 @@ QA_DEVICE void quant_vt(const _Float16* __restrict__ v, int8_t* __restrict__ vi,
   const int h = lane >> 5, c = lane & 31;
   const long row = blk * 32 + c;
   v8h x[NDB][2];
-  float amax = 0.f;
+  v2us am = {0, 0};
 #pragma unroll
   for (int b = 0; b < NDB; ++b)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       x[b][u] = *reinterpret_cast<const v8h*>(v + row * D + 32 * b + 16 * h + 8 * u);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf((float)x[b][u][j]));
+      amax_pk8(x[b][u], am);
     }
-  amax = wave_max_f(amax);
+  const float amax = wave_max_f(amax_pk_f32(am));
   const _Float16 s16 = (_Float16)(amax / 127.0f);
   const float s = (float)s16;
   const float r = quant_rcp(s);
@@ -129,25 +150,6 @@ __global__ __launch_bounds__(256) void quant_vt_kernel(const _Float16* __restric
   const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blk >= nblocks) return;
   quant_vt<D>(v, vi, sv, vt, blk, threadIdx.x & 63);
-}
-// k and v of one forward in one launch: workgroups alternate between 4 k blocks (the quantiser,
-// with the k-mean smoothing and the backward's bf16 image as asked) and 4 v blocks (v_i8, sv and the
-// P.V operand image), so the two streams share the machine from the first to the last wave and pay
-// one launch ramp instead of two.
-template <int D, bool SMOOTH, bool IMG>
-__global__ __launch_bounds__(256) void quant_kv_kernel(
-    const _Float16* __restrict__ k, int8_t* __restrict__ ki, _Float16* __restrict__ sk,
-    __bf16* __restrict__ kimg, const _Float16* __restrict__ kmean, const _Float16* __restrict__ v,
-    int8_t* __restrict__ vi, _Float16* __restrict__ sv, int8_t* __restrict__ vt, long nblocks,
-    int rows_per_head) {
-  const long wg = blockIdx.x >> 1;
-  const long blk = wg * 4 + (threadIdx.x >> 6);
-  if (blk >= nblocks) return;
-  if (blockIdx.x & 1)
-    quant_vt<D>(v, vi, sv, vt, blk, threadIdx.x & 63);
-  else
-    quant_block32<D, false, SMOOTH, IMG>(k, ki, sk, nullptr, kimg, kmean, blk, rows_per_head,
-                                         threadIdx.x & 63);
 }
 // vt from stored indices (an int8 key/value cache restored from its wire format, kv_cache.py)
 template <int D>
@@ -262,29 +264,6 @@ extern "C" int qattn_int8_quant_vt(const void* v, void* v_i8, void* sv, void* vt
   else
     hipLaunchKernelGGL(quant_vt_kernel<64>, grid, block, 0, st, (const _Float16*)v, (int8_t*)v_i8,
                        (_Float16*)sv, (int8_t*)vt, nblocks);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
-extern "C" int qattn_int8_quant_kv(const void* k, void* k_i8, void* sk, void* k_img, const void* kmean,
-                                   const void* v, void* v_i8, void* sv, void* vt, long rows,
-                                   int rows_per_head, int head_dim, void* stream) {
-  if (rows % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
-  if (kmean && rows_per_head % 32 != 0) return 1;
-  const long nblocks = rows / 32;
-  if (nblocks == 0) return 0;
-  dim3 grid((unsigned)(2 * ((nblocks + 3) / 4))), block(256);
-  hipStream_t st = (hipStream_t)stream;
-#define QA_KV(Dv, SM, IM)                                                                          \
-  hipLaunchKernelGGL((quant_kv_kernel<Dv, SM, IM>), grid, block, 0, st, (const _Float16*)k,        \
-                     (int8_t*)k_i8, (_Float16*)sk, (__bf16*)k_img, (const _Float16*)kmean,          \
-                     (const _Float16*)v, (int8_t*)v_i8, (_Float16*)sv, (int8_t*)vt, nblocks,        \
-                     rows_per_head)
-#define QA_KV_D(Dv)                                                                                \
-  if (kmean) { if (k_img) QA_KV(Dv, true, true); else QA_KV(Dv, true, false); }                   \
-  else { if (k_img) QA_KV(Dv, false, true); else QA_KV(Dv, false, false); }
-  if (head_dim == 128) { QA_KV_D(128) } else { QA_KV_D(64) }
-#undef QA_KV_D
-#undef QA_KV
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -169,9 +169,9 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
   }
 
   const float qks = qk_scale(D);
-  call(qattn_int8_quant_kv(P(k), P(k_i8), P(sk), nullptr, P(k_mean), P(v), P(v_i8), P(sv), P(vt), Nkv,
-                           (int)Sk, (int)D, c.stream),
-       "quantise k, v");
+  call(qattn_int8_quant(P(k), P(k_i8), P(sk), nullptr, P(k_mean), Nkv, (int)Sk, (int)D, c.stream),
+       "quantise k");
+  call(qattn_int8_quant_vt(P(v), P(v_i8), P(sv), P(vt), Nkv, (int)D, c.stream), "quantise v");
   call(qattn_int8_attn_fwd_qf(P(q), P(q_i8), P(sq), nullptr, P(k_i8), P(sk), P(vt), P(sv), P(O), P(lse),
                               B * H, S, Sk, (int)(H / Hkv), causal ? 1 : 0, (int)D, qks, c.stream),
        "int8 forward");

@@ -227,35 +227,3 @@ def test_int8_fwd_q_fused_bit_identical(lib, shape, causal, G):
     for a, b_ in zip(*outs):
         assert torch.equal(a.view(torch.uint8) if a.dtype == torch.int8 else a.view(torch.int16),
                            b_.view(torch.uint8) if b_.dtype == torch.int8 else b_.view(torch.int16))
-
-
-@pytest.mark.parametrize("D,smooth,img", [(128, True, True), (64, False, False), (128, False, True)])
-def test_int8_quant_kv_bit_identical(lib, D, smooth, img):
-    """qattn_int8_quant_kv (k and v in one launch) equals qattn_int8_quant_img on k and
-    qattn_int8_quant_vt on v bit for bit."""
-    from quantizedattention_amd import _lib
-    B, H, S = 2, 3, 224
-    g = torch.Generator().manual_seed(22)
-    k, v = ((torch.randn((B, H, S, D), generator=g) * 4).half().cuda() for _ in range(2))
-    v[0, 1, 64:96] = 0
-    N = B * H * S
-    e = lambda *s_, dt: torch.zeros(s_, dtype=dt, device="cuda")  # noqa: E731
-    st, P = _lib.stream_of(k), _lib.ptr
-    km = e(B * H, D, dt=torch.float16) if smooth else None
-    if smooth:
-        _lib.call("qattn_kmean", P(k), P(km), B * H, S, D, st)
-    res = []
-    for fused in (False, True):
-        ki, vi, vt = e(N, D, dt=torch.int8), e(N, D, dt=torch.int8), e(N, D, dt=torch.int8)
-        sk, sv = e(N // 32, dt=torch.float16), e(N // 32, dt=torch.float16)
-        kb = e(N, D, dt=torch.bfloat16) if img else None
-        if fused:
-            _lib.call("qattn_int8_quant_kv", P(k), P(ki), P(sk), P(kb), P(km), P(v), P(vi), P(sv), P(vt),
-                      N, S, D, st)
-        else:
-            _lib.call("qattn_int8_quant_img", P(k), P(ki), P(sk), None, P(kb), P(km), N, S, D, st)
-            _lib.call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
-        res.append([t for t in (ki, sk, kb, vi, sv, vt) if t is not None])
-    torch.cuda.synchronize()
-    for a, b_ in zip(*res):
-        assert torch.equal(a, b_)

@@ -54,9 +54,25 @@ def t(f, reps=15):
     return sorted(ts)[reps // 2]
 
 
+causal = os.environ.get("QATTN_AB_CAUSAL") == "1"
+if causal:   # the whole record backward, causal (dK+dV then dQ in one call)
+    lib.qattn_int8_attn_bwd_ws.argtypes = SIGNATURES["qattn_int8_attn_bwd_ws"]
+    f1 = lambda: lib.qattn_int8_attn_bwd_ws(P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv),  # noqa: E731
+                                            P(LD), P(qb), P(kb), P(ob), P(dq), P(dk), P(dv), P(ws), bh,
+                                            S, S, 1, 1, D, qks, sms, st)
+    f2 = lambda: 0  # noqa: E731
 t1, t2 = t(f1), t(f2)
+if os.environ.get("QATTN_AB_SAVE"):   # outputs for a numeric comparison across builds
+    torch.save({"dk": dk.cpu(), "dv": dv.cpu(), "dq": dq.cpu()}, os.environ["QATTN_AB_SAVE"])
+if os.environ.get("QATTN_AB_REF"):
+    ref = torch.load(os.environ["QATTN_AB_REF"], weights_only=True)
+    for n_, x in (("dk", dk), ("dv", dv), ("dq", dq)):
+        r = ref[n_].float()
+        d = (x.cpu().float() - r).abs()
+        print(f"  {n_}: max|diff| {d.max().item():.3g} (max|ref| {r.abs().max().item():.3g}), "
+              f"identical {bool(torch.equal(x.cpu(), ref[n_]))}", flush=True)
 h = hashlib.sha256()
 for x in (dk, dv, dq):
     h.update(x.view(torch.int16).cpu().numpy().tobytes())
-print(f"{os.path.basename(path)}: dK+dV {t1:.1f} us, dQ from records {t2:.1f} us, outputs "
+print(f"{os.path.basename(path)}{' causal' if causal else ''}: dK+dV {t1:.1f} us, dQ from records {t2:.1f} us, outputs "
       f"{h.hexdigest()[:12]}", flush=True)
