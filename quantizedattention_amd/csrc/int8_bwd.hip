@@ -664,8 +664,10 @@ void int8_bwd_kernel(
       // before the store read it: dword 0 of some records of the last query tile came out wrong,
       // run-dependently, at D = 64 (tools/nondet_probe3.py; tests/test_gpu_int8_ext.py::
       // test_int8_bwd_ws_long_d64; tests/test_isa.py checks the emitted code).
+      // (slot of lane l: l ^ 4(l >> 5), so the dQ pass's transposed reads of two slot halves fall on
+      // different banks, int8_bwd_dqw_kernel)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, bytes), ws_rsrc,
-                                             16 * lane + (int)(rel * 1024u), 0, 0);
+                                             16 * (lane ^ ((lane >> 5) << 2)) + (int)(rel * 1024u), 0, 0);
       (void)nqt;
       if (lane == 0) sds_lds[wave * nt + t] = sx;   // written out after the loop
     }
@@ -838,6 +840,13 @@ void int8_bwd_kernel(
 #ifndef QA_DQW_NT
 #define QA_DQW_NT 1
 #endif
+// QA_DQW_TR8 (A/B): the record read as two ds_read_b64_tr_b8 straight into dQ order (1) instead of
+// one 16-B read and the permutation MFMA (0).  Bit-identical dq, 92 instead of 115 VGPRs, one MFMA
+// fewer per tile-wave -- and measured no faster: 162-171 against 156-165 us per 32-head chunk at
+// config 3 (profiles/r05_dqw_tr8_ab.log; the kernel is bound by the record stream).
+#ifndef QA_DQW_TR8
+#define QA_DQW_TR8 0
+#endif
 #ifndef QA_DQW_NSLOT
 #define QA_DQW_NSLOT 4
 #endif
@@ -927,6 +936,20 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
     for (int i = lane; i < nt; i += 64) sds_lds[wave * nkt + i] = sds[rec0 + i];
   for (int i = tid; i < nt; i += 64 * W::WAVES) sk_lds[i] = sk[kv_row0 / 32 + i];
 
+#if QA_DQW_TR8
+  // ds_read_b64_tr_b8 of the record (per 16-lane group: lane 2j+p reads bytes 8p..8p+7 of row j,
+  // lane i receives byte i of the 8 rows): rows = the record slots (key on the row) of the 8 keys of
+  // this lane's B-operand k-step, in the k order of the k image's A operand (key 16s + 8(j >> 2) +
+  // 4h + (j & 3)); the slot half (lane >> 4) & 1 picks the queries: lane l receives query
+  // qcol(l & 31) = 8((c & 15) >> 2) + 4(c >> 4) + (c & 3) of the record's byte order, and the
+  // epilogue stores column c to that row.  No permutation MFMA; the same products in the same order.
+  int rtr;
+  {
+    const int j = (lane & 15) >> 1;
+    const int hq = (lane >> 4) & 1;   // record slot key + 32 hq, stored at (key ^ 4hq) + 32 hq
+    rtr = 16 * (((8 * (j >> 2) + 4 * h + (j & 3)) ^ (4 * hq)) + 32 * hq) + 8 * (lane & 1);
+  }
+#else
   // permutation operand: byte i of lane l is 1 iff query 8(i/4) + 4(l/32) + i%4 is this lane's
   // column l%32 (one byte in the lane half that holds it)
   v4i perm = {0, 0, 0, 0};
@@ -934,6 +957,7 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
     const int i = 4 * (c32 >> 3) + (c32 & 3);
     perm[i >> 2] = 1 << (8 * (i & 3));
   }
+#endif
   int troff[C::NDB];
   {
     const int gg = (lane >> 4) & 1, i16 = lane & 15;
@@ -951,10 +975,25 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
   // the bf16 operand of tile t: its record brought into dQ order by the permutation MFMA (exact
   // integers), scaled by s_dS * sk
   auto make_op = [&](int t, v8bf* op) {
-    const v4i rec = *reinterpret_cast<const v4i*>(smem + W::RBASE + (t % W::RSLOT) * W::REC +
-                                                  wave * 1024 + 16 * lane);
-    const v16i x = mfma_i8(rec, perm, v16i{});   // dS_i8 in dQ order (exact integers)
     const float c = sds_lds[wave * nkt + t] * (float)sk_lds[t];
+#if QA_DQW_TR8
+    const char* rb = smem + W::RBASE + (t % W::RSLOT) * W::REC + wave * 1024 + rtr;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const v2i x = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+          (__attribute__((address_space(3))) v2i*)(rb + 256 * s));   // keys 16s .. 16s + 15
+      v4u w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int wd = x[j >> 1], sh = 16 * (j & 1);
+        w[j] = pk_bf16((float)(signed char)(wd >> sh) * c, (float)(signed char)(wd >> (sh + 8)) * c);
+      }
+      op[s] = __builtin_bit_cast(v8bf, w);
+    }
+#else
+    const v4i rec = *reinterpret_cast<const v4i*>(smem + W::RBASE + (t % W::RSLOT) * W::REC +
+                                                  wave * 1024 + 16 * (lane ^ ((lane >> 5) << 2)));
+    const v16i x = mfma_i8(rec, perm, v16i{});   // dS_i8 in dQ order (exact integers)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       v4u w;
@@ -963,6 +1002,7 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
         w[j] = pk_bf16((float)x[8 * s + 2 * j] * c, (float)x[8 * s + 2 * j + 1] * c);
       op[s] = __builtin_bit_cast(v8bf, w);
     }
+#endif
   };
 
   vmem_drain();
@@ -1002,7 +1042,11 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
   }
   vmcnt_wait_all();
   if (!active) return;
+#if QA_DQW_TR8
+  const long r = (long)bh * Sq + q0 + 8 * ((c32 & 15) >> 2) + 4 * (c32 >> 4) + (c32 & 3);
+#else
   const long r = (long)bh * Sq + q0 + c32;
+#endif
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) {
 #pragma unroll
