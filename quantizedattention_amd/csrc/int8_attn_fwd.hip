@@ -88,6 +88,11 @@ struct SmTile {
 #ifndef QA_FWD_UNROLL
 #define QA_FWD_UNROLL 1
 #endif
+// QA_FWD_UNROLL_CAUSAL (A/B): the ring-slot unroll in the causal instantiations too (their
+// mask-free tiles before the diagonal band)
+#ifndef QA_FWD_UNROLL_CAUSAL
+#define QA_FWD_UNROLL_CAUSAL 1
+#endif
 // Timing-only ablations of the ring skeleton (-DQA_FWD_ABL=N, tools/ab_time.py; wrong results):
 // 1 no wait+barrier on odd tiles of the unrolled group, 2 also one DMA issue (2 tiles) per 2 tiles,
 // 3 no DMA after the prologue, 4 no wait+barrier in the loop
@@ -577,7 +582,7 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
     // groups of NSLOT = 4 tiles with compile-time ring slots (immediate LDS offsets, one 16-B read
     // of each scale table per group), then the remaining tiles with run-time slots
     static_assert(C::NSLOT == 4, "ring of 4 slots");
-    constexpr bool UNROLL = QA_FWD_UNROLL && !CAUSAL && (QF || FIX || SPLIT);
+    constexpr bool UNROLL = QA_FWD_UNROLL && (!CAUSAL || QA_FWD_UNROLL_CAUSAL) && (QF || FIX || SPLIT);
     const std::false_type nodiag{};
     int t = 0;
     for (; UNROLL && t + 4 <= tmain; t += 4) {

@@ -40,9 +40,19 @@ P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
 sms = float(torch.tensor(1 / math.sqrt(D), dtype=torch.float32))
+causal = os.environ.get("CAUSAL") == "1"
+if causal:   # the causal record backward in one pass (dK+dV stamped, then dQ from the records)
+    full = lib.qattn_int8_attn_bwd_ws
+    full.argtypes = SIGNATURES["qattn_int8_attn_bwd_ws"]
+    kb = ki.bfloat16()
+    dq = torch.empty((N, D), dtype=torch.float16, device="cuda")
 for _ in range(int(os.environ.get("REPS", "3"))):   # launches before the stamped (last) one
-    rc = fn(P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD), P(qb), P(ob), P(dk), P(dv),
-            P(ws), bh, S, D, qks, sms, st)
+    if causal:
+        rc = full(P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD), P(qb), P(kb), P(ob),
+                  P(dq), P(dk), P(dv), P(ws), bh, S, S, 1, 1, D, qks, sms, st)
+    else:
+        rc = fn(P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv), P(LD), P(qb), P(ob), P(dk), P(dv),
+                P(ws), bh, S, D, qks, sms, st)
     assert rc == 0
 torch.cuda.synchronize()
 buf = np.zeros((4096, 4), dtype=np.uint64)
@@ -56,6 +66,11 @@ print(f"{nwg} workgroups, kernel span {us[:, 3].max():.1f} us")
 for name, x in (("prologue", pro), ("tile loop", loop), ("epilogue", epi), ("start", us[:, 0]),
                 ("end", us[:, 3])):
     print(f"  {name:9s} min {x.min():7.1f}  median {np.median(x):7.1f}  max {x.max():7.1f} us")
+busy = (us[:, 3] - us[:, 0]).sum()
+print(f"  workgroup-time {busy:.0f} us over 256 CUs: {busy / 256:.1f} us per CU if perfectly packed "
+      f"({busy / 256 / us[:, 3].max() * 100:.1f} % of the span)")
+ends = np.sort(us[:, 3])
+print("  last ends (us):", np.round(ends[-8:], 1).tolist(), " 90th pct end", round(float(np.percentile(ends, 90)), 1))
 order = np.argsort(us[:, 0])
 starts = us[order, 0]
 print("  start-time histogram (us):", np.histogram(starts, bins=8)[0].tolist(),
