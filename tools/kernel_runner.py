@@ -33,9 +33,8 @@ qks = float(torch.tensor(1 / math.sqrt(D) * 1.44269504, dtype=torch.float32))
 sms = float(torch.tensor(1 / math.sqrt(D), dtype=torch.float32))
 O, lse, qi, kiT, vi, sq, sk, sv, km, _, _ = _int8_forward(q, k, v, False)
 ki = kiT.t()
-vdq = torch.empty((N, D), dtype=torch.float16, device="cuda")
-_lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
 vt = torch.empty((N, D), dtype=torch.int8, device="cuda")
+qi2, sq2 = torch.empty_like(qi), torch.empty_like(sq)
 _lib.call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st)
 dOi = torch.empty((N, D), dtype=torch.int8, device="cuda")
 sdO = torch.empty((N // 32,), dtype=torch.float16, device="cuda")
@@ -53,8 +52,16 @@ if name.startswith("bf16"):
     Ob, lseb = helion_atten_bf16_fwd_training(q, k, vb, False)
 torch.cuda.synchronize()
 for name in [n for _ in range(reps) for n in names]:
-    if name == "int8_fwd":
-        _lib.call("qattn_int8_attn_fwd", P(qi), P(sq), P(ki), P(sk), P(vdq), P(O), P(lse), B * H, S, D, qks, st)
+    if name == "int8_fwd":   # the forward the drop-ins run: q quantised in the kernel, with its fixup
+        _lib.call("qattn_int8_attn_fwd_qf", P(q), P(qi2), P(sq2), None, P(ki), P(sk), P(vt), P(sv), P(O),
+                  P(lse), B * H, S, S, 1, 0, D, qks, st)
+    elif name == "int8_fwd_causal":
+        _lib.call("qattn_int8_attn_fwd_qf", P(q), P(qi2), P(sq2), None, P(ki), P(sk), P(vt), P(sv), P(O),
+                  P(lse), B * H, S, S, 1, 1, D, qks, st)
+    elif name == "int8_bwd_causal":   # the causal record backward in one call (dK+dV, then dQ)
+        _lib.call("qattn_int8_attn_bwd_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv),
+                  P(LD), P(qb), P(kb), P(ob), P(dq), P(dk), P(dv), P(ws), B * H, S, S, 1, 1, D, qks, sms,
+                  st)
     elif name == "int8_fwd_i8":
         _lib.call("qattn_int8_attn_fwd_ex", P(qi), P(sq), P(ki), P(sk), P(vt), P(sv), P(O), P(lse),
                   B * H, S, S, 1, 0, D, qks, st)
@@ -85,6 +92,6 @@ for name in [n for _ in range(reps) for n in names]:
         qq = q[:2, :16, :2048].contiguous().bfloat16()
         helion_attention_jvp_forward_fp32(qq, qq, qq, qq, qq, qq)
     elif name == "quant":
-        _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), P(vdq), None, N, S, D, st)
+        _lib.call("qattn_int8_quant", P(v), P(vi), P(sv), None, None, N, S, D, st)
 torch.cuda.synchronize()
 print("done", sys.argv[1], reps)
