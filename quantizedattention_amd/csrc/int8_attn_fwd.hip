@@ -105,7 +105,7 @@ struct SmTile {
 #define QA_FWD_LIT_COUNT 0
 #endif
 #if QA_FWD_LIT_COUNT
-__device__ unsigned long long g_fwd_lit[2];
+__device__ unsigned long long g_fwd_lit[4];   // literal wave-tiles, wave-tiles, marked waves, waves
 #endif
 #if QA_FWD_STAMP
 __device__ unsigned long long g_fwd_stamp[8192][4];
@@ -631,6 +631,12 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
       fix = __ballot(any) != 0;
     }
   }
+#if QA_FWD_LIT_COUNT
+  if (DEFER && lane == 0) {
+    atomicAdd(&g_fwd_lit[3], 1ull);
+    if (fix) atomicAdd(&g_fwd_lit[2], 1ull);
+  }
+#endif
   if constexpr (SPLIT) {   // the partial state of this key range: {m, l} and f16(O / l)
     l = pair_sum(l);
     const long prow = ((long)split * BH + bh) * Sq + q0;

@@ -99,7 +99,8 @@ for mode, f in fns.items():
     cnt = getattr(lib, "qattn_fwd_lit_count", None)
     if cnt is not None:   # -DQA_FWD_LIT_COUNT=1 builds: literal tiles per wave-tile since load
         import numpy as np
-        buf = np.zeros(2, dtype=np.uint64)
+        buf = np.zeros(4, dtype=np.uint64)
         cnt.argtypes = [ctypes.c_void_p]
         cnt(buf.ctypes.data)
-        print(f"  literal wave-tiles {int(buf[0])} of {int(buf[1])} ({100 * buf[0] / max(1, buf[1]):.2f} %)")
+        print(f"  literal wave-tiles {int(buf[0])} of {int(buf[1])} ({100 * buf[0] / max(1, buf[1]):.2f} %), "
+              f"waves marked for the fixup {int(buf[2])} of {int(buf[3])} ({100 * buf[2] / max(1, buf[3]):.3f} %)")
