@@ -338,7 +338,12 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) o[b] = v16f{};
   _Float16 m = (_Float16)(-INFINITY);
-  _Float16 m_thr = (_Float16)(-INFINITY);   // m + THR (f16): the deferred running max moves past it
+  // f16(m + THR): the deferred running max moves when a row's tile max exceeds it.  (The f16 sum can
+  // round up, so a tile max equal to that rounded value leaves m in place where an fp32 compare would
+  // move it: er = exp2(rm - m) then exceeds 2^THR by at most half an f16 ulp of m + THR.  er only
+  // scales l and the P.V factor -- P itself is taken against the tile max -- so O and lse stay within
+  // rounding of each other either way, but bits can differ from an fp32-compare build.)
+  _Float16 m_thr = (_Float16)(-INFINITY);
   _Float16 mt = (_Float16)(-INFINITY);      // the reference's (undeferred) running max
   float l = 0.f;      // per-lane partial (this lane's key half); the reference's l = 1 is wiped by r = 0
   float obias = 0.f;  // sum of the tile dequantisation factors (the KMAG bias of O is KMAG * obias)
