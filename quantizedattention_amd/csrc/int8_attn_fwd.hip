@@ -197,15 +197,19 @@ QA_DEVICE LitOut literal_chain(const v16i& acc, int mx, float cq, float skt, flo
 constexpr unsigned short FIX_LSE16 = 0x7e5au;    // an fp16 NaN no result carries
 constexpr unsigned FIX_M32 = 0x7fc0e5a5u;        // an fp32 NaN no result carries
 
-template <int D, bool CAUSAL, bool SPLIT = false, bool QF = false, bool FIX = false>
-__global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_kernel(
+// The kernel body.  INL (the inline fixup): the marks travel through mark_lds, WAVES words in LDS,
+// instead of the lse sentinel; the fast pass and the fixup pass run in one workgroup (see
+// int8_attn_fwd_kernel).
+template <int D, bool CAUSAL, bool SPLIT, bool QF, bool FIX, bool INL>
+QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
     const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
     const _Float16* __restrict__ sk, const int8_t* __restrict__ vt, const _Float16* __restrict__ sv,
     _Float16* __restrict__ out, _Float16* __restrict__ lse, int BH, int Sq, int Sk, int G, int qoff,
-    float qks, const _Float16* __restrict__ q16, __bf16* __restrict__ qbf) {
+    float qks, const _Float16* __restrict__ q16, __bf16* __restrict__ qbf, unsigned* mark_lds) {
   static_assert(!SPLIT || !CAUSAL, "key splits: non-causal");
   static_assert(!SPLIT || !QF, "key splits: pre-quantised q");
-  static_assert(!FIX || !QF, "the fixup reads the q_i8 the forward wrote");
+  static_assert(!FIX || !QF || INL, "the separate fixup reads the q_i8 the forward wrote");
+  static_assert(!INL || !SPLIT, "the inline fixup: the non-split forward");
   using C = Int8FwdCfg<D>;
   constexpr bool DEFER = C::LIT_K > 0 && QA_FWD_DEFER > 0 && !FIX;
   FWD_STAMP(0);
@@ -233,7 +237,9 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
       const int r0 = qt * C::QROWS + w * 32;
       bool f = false;
       if (r0 < Sq) {
-        if constexpr (SPLIT)
+        if constexpr (INL)
+          f = mark_lds[w] != 0;
+        else if constexpr (SPLIT)
           f = __float_as_uint(reinterpret_cast<const float2*>(lse)[((long)split * BH + bh) * Sq + r0].x) ==
               FIX_M32;
         else
@@ -655,9 +661,10 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   // ---------------- epilogue: lse = fp16(m + fp16(log2 l)); O = fp16(O / l)   (int8:252-257)
   l = pair_sum(l);
   const long qrow = head_row0 + q0 + c32;
+  if (INL && fix && lane == 0) mark_lds[wave] = 1u;
   if (h == 0)
-    lse[qrow] = fix ? __builtin_bit_cast(_Float16, FIX_LSE16)
-                    : (_Float16)((float)m + (float)(_Float16)log2_f32(l));
+    lse[qrow] = (fix && !INL) ? __builtin_bit_cast(_Float16, FIX_LSE16)
+                              : (_Float16)((float)m + (float)(_Float16)log2_f32(l));
   const float inv = 1.0f / l;
   store_rows<D, _Float16, 1, true>(o, inv, smem + wave * RowTile<D, _Float16>::BYTES,
                                    out + (head_row0 + q0) * D, lane, -KMAG * obias * inv);
@@ -665,6 +672,39 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   FWD_STAMP(3);
 #endif
+}
+
+// QA_FWD_INLINE_FIX (A/B): the non-split forward redoes its marked waves in the same workgroup, right
+// after the fast pass (a second, literal-chain pass over the tiles, with q quantised again from q16),
+// instead of in a second launch
+#ifndef QA_FWD_INLINE_FIX
+#define QA_FWD_INLINE_FIX 1
+#endif
+template <int D, bool CAUSAL, bool SPLIT = false, bool QF = false, bool FIX = false, bool INL = false>
+__global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_kernel(
+    const int8_t* __restrict__ q_i8, const _Float16* __restrict__ sq, const int8_t* __restrict__ k_i8,
+    const _Float16* __restrict__ sk, const int8_t* __restrict__ vt, const _Float16* __restrict__ sv,
+    _Float16* __restrict__ out, _Float16* __restrict__ lse, int BH, int Sq, int Sk, int G, int qoff,
+    float qks, const _Float16* __restrict__ q16, __bf16* __restrict__ qbf) {
+  if constexpr (!INL) {
+    int8_attn_fwd_body<D, CAUSAL, SPLIT, QF, FIX, false>(q_i8, sq, k_i8, sk, vt, sv, out, lse, BH, Sq, Sk, G,
+                                                         qoff, qks, q16, qbf, nullptr);
+  } else {
+    using C = Int8FwdCfg<D>;
+    extern __shared__ __attribute__((aligned(16))) char smem_k[];
+    // after the body's LDS regions for any workgroup (sized for all key tiles)
+    unsigned* marks = reinterpret_cast<unsigned*>(smem_k + C::lds_bytes(Sk / C::KT));
+    if (threadIdx.x < C::WAVES) marks[threadIdx.x] = 0u;   // (published by the body's first barrier)
+    int8_attn_fwd_body<D, CAUSAL, false, QF, false, true>(q_i8, sq, k_i8, sk, vt, sv, out, lse, BH, Sq, Sk,
+                                                          G, qoff, qks, q16, qbf, marks);
+    __syncthreads();
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < C::WAVES; ++w) any = any || marks[w] != 0u;
+    if (any)
+      int8_attn_fwd_body<D, CAUSAL, false, QF, true, true>(q_i8, sq, k_i8, sk, vt, sv, out, lse, BH, Sq, Sk,
+                                                           G, qoff, qks, q16, qbf, marks);
+  }
 }
 
 template <int D, bool CAUSAL, bool QF>
@@ -675,13 +715,16 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
   using C = Int8FwdCfg<D>;
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int lds = C::lds_bytes((int)(sk_tok / 32));
-  auto kern = int8_attn_fwd_kernel<D, CAUSAL, false, QF>;
-  { static int granted_ = 0; if (!lds_grant((const void*)kern, lds, granted_)) return 1; }
-  hipLaunchKernelGGL(kern, dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds, st,
+  // the inline fixup (q quantised in the kernel: the fixup pass quantises it again from q16)
+  constexpr bool INL = QA_FWD_INLINE_FIX && QF && C::LIT_K > 0 && QA_FWD_DEFER;
+  auto kern = int8_attn_fwd_kernel<D, CAUSAL, false, QF, false, INL>;
+  const int lds_k = lds + (INL ? 4 * C::WAVES : 0);
+  { static int granted_ = 0; if (!lds_grant((const void*)kern, lds_k, granted_)) return 1; }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds_k, st,
                      (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
                      (const int8_t*)vt, (const _Float16*)sv, (_Float16*)out, (_Float16*)lse, (int)bh,
                      (int)sq_tok, (int)sk_tok, group, qoff, qks, (const _Float16*)q16, (__bf16*)qbf);
-  if constexpr (C::LIT_K > 0 && QA_FWD_DEFER) {   // the waves whose first tile must be redone
+  if constexpr (C::LIT_K > 0 && QA_FWD_DEFER && !INL) {   // the waves whose votes held: redone
     auto fixk = int8_attn_fwd_kernel<D, CAUSAL, false, false, true>;
     { static int granted_ = 0; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
     hipLaunchKernelGGL(fixk, dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds, st,
