@@ -148,7 +148,7 @@ def int8_kernel_times(q, k, v, dO, n):
         "quant_block32_kernel(k, fwd)": lambda: _lib.call("qattn_int8_quant", P(k), P(ki), P(sk), None,
                                                           P(km), N, S, D, st),
         # the forward the drop-ins run (q quantised in its prologue; P.V on the int8 MFMA, the
-        # reference's hl.dot(P_i8, v_i8)), with its fixup launch (int8_attn_fwd.hip DEFER0)
+        # reference's hl.dot(P_i8, v_i8)), its fixup pass inline (int8_attn_fwd.hip)
         "int8_attn_fwd_kernel": lambda: _lib.call("qattn_int8_attn_fwd_qf", P(q), P(qi), P(sq), None,
                                                   P(ki), P(sk), P(vt), P(sv), P(O), P(lse), B * H, S,
                                                   S, 1, 0, D, qks, st),

@@ -85,8 +85,9 @@ int qattn_int8_attn_fwd(const void* q_i8, const void* sq, const void* k_i8, cons
  * are excluded.  Block scales index the
  * query rows and the key/value rows separately.  sq_tok % 32 == sk_tok % 32 == 0, bh % group == 0.
  * qattn_int8_attn_fwd is this with sq_tok = sk_tok = seq, group = 1, causal = 0.
- * Every int8 forward entry enqueues two kernels on `stream`: the attention kernel, then a fixup
- * kernel that recomputes the waves whose literal-P-chain vote held at the end. */
+ * The forward marks the (rare) waves whose literal-P-chain vote still holds at the end and redoes
+ * them: qattn_int8_attn_fwd_qf in the same kernel, the entries on pre-quantised q
+ * (and the split entry) with a second kernel on `stream`. */
 int qattn_int8_attn_fwd_ex(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
                            const void* vt, const void* sv, void* out, void* lse, long bh,
                            long sq_tok, long sk_tok, int group, int causal, int head_dim,
