@@ -608,6 +608,21 @@ QA_DEVICE void xcd_remap_lpt(int bid, int nq, int nbh, bool heavy_last, int& bh,
   qt = heavy_last ? nq - 1 - r : r;
 }
 
+// xcd_remap_lpt over groups of hg heads per XCD: the groups run one after another, longest-first
+// inside a group.  Fewer heads in flight per XCD (hg instead of nbh / 8) keep the blocks of one head
+// that stream the same rows close together in time, for L2 reuse.  hg must divide nbh / 8.
+QA_DEVICE void xcd_remap_lpt_grouped(int bid, int nq, int nbh, bool heavy_last, int hg, int& bh, int& qt) {
+  if ((nbh & 7) != 0 || ((nbh >> 3) % hg) != 0) {
+    xcd_remap_lpt(bid, nq, nbh, heavy_last, bh, qt);
+    return;
+  }
+  const int xcd = bid & 7, j = bid >> 3;
+  const int g = j / (hg * nq), k = j % (hg * nq);
+  const int r = k / hg;
+  bh = (g * hg + k % hg) * 8 + xcd;
+  qt = heavy_last ? nq - 1 - r : r;
+}
+
 // Workgroup -> (head, q-tile) remap that keeps every q-tile of one head on one XCD
 // (blocks b and b+8 share an XCD under round-robin dispatch; speed only, never correctness).
 QA_DEVICE void xcd_remap(int bid, int nq, int nbh, int& bh, int& qt) {

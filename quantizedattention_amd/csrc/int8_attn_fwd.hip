@@ -88,6 +88,11 @@ struct SmTile {
 #ifndef QA_FWD_UNROLL
 #define QA_FWD_UNROLL 1
 #endif
+// QA_FWD_HG (A/B): causal grid order -- longest-first within groups of this many heads per XCD
+// (0: longest-first over all heads)
+#ifndef QA_FWD_HG
+#define QA_FWD_HG 0
+#endif
 // QA_FWD_UNROLL_CAUSAL (A/B): the ring-slot unroll in the causal instantiations too (their
 // mask-free tiles before the diagonal band)
 #ifndef QA_FWD_UNROLL_CAUSAL
@@ -219,7 +224,8 @@ QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
 
   const int nq = (Sq + C::QROWS - 1) / C::QROWS;
   int bh, qt;
-  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nq, BH, true, bh, qt);
+  if constexpr (CAUSAL && QA_FWD_HG > 0) xcd_remap_lpt_grouped(blockIdx.x, nq, BH, true, QA_FWD_HG, bh, qt);
+  else if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nq, BH, true, bh, qt);
   else xcd_remap(blockIdx.x, nq, BH, bh, qt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -208,6 +208,14 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #define QA_DKV_NSLOT 4
 #endif
 // cache policy of the dS record stores (builtin aux: 2 = nt, 16 = sc1)
+// QA_DKV_HG: causal fused dK+dV grid order -- longest-first within groups of this many heads
+// per XCD (0: longest-first over all heads, xcd_remap_lpt)
+#ifndef QA_DKV_HG
+#define QA_DKV_HG 4
+#endif
+#ifndef QA_DQW_HG   // (the same for the causal dQ-from-records grid)
+#define QA_DQW_HG 0
+#endif
 #ifndef QA_BWD_PACK_ASM
 #define QA_BWD_PACK_ASM 1
 #endif
@@ -398,7 +406,9 @@ void int8_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nxb = (Sx + G::XROWS - 1) / G::XROWS;
   int bh, xt;
-  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nxb, BH, ROLE == ROLE_DQ, bh, xt);
+  if constexpr (CAUSAL && ROLE == ROLE_DKV && QA_DKV_HG > 0)
+    xcd_remap_lpt_grouped(blockIdx.x, nxb, BH, false, QA_DKV_HG, bh, xt);
+  else if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nxb, BH, ROLE == ROLE_DQ, bh, xt);
   else xcd_remap(blockIdx.x, nxb, BH, bh, xt);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -884,7 +894,8 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = (Sq + 32 * W::WAVES - 1) / (32 * W::WAVES);
   int bh, qb;
-  if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nqb, BH, true, bh, qb);
+  if constexpr (CAUSAL && QA_DQW_HG > 0) xcd_remap_lpt_grouped(blockIdx.x, nqb, BH, true, QA_DQW_HG, bh, qb);
+  else if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nqb, BH, true, bh, qb);
   else xcd_remap(blockIdx.x, nqb, BH, bh, qb);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -19,7 +19,7 @@ lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 for n in ("qattn_int8_bwd_dkdv_ws", "qattn_int8_bwd_dq_ws", "qattn_int8_bwd_ws_bytes"):
     getattr(lib, n).argtypes = SIGNATURES[n]
 lib.qattn_int8_bwd_ws_bytes.restype = ctypes.c_long
-bh, S, D = 32, 4096, 128
+bh, S, D = int(os.environ.get("BH", "32")), 4096, 128
 N = bh * S
 g = torch.Generator(device="cuda").manual_seed(0)
 i8 = lambda: torch.randint(-127, 128, (N, D), device="cuda", generator=g, dtype=torch.int8)  # noqa: E731

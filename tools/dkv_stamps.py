@@ -71,6 +71,20 @@ print(f"  workgroup-time {busy:.0f} us over 256 CUs: {busy / 256:.1f} us per CU 
       f"({busy / 256 / us[:, 3].max() * 100:.1f} % of the span)")
 ends = np.sort(us[:, 3])
 print("  last ends (us):", np.round(ends[-8:], 1).tolist(), " 90th pct end", round(float(np.percentile(ends, 90)), 1))
+if causal:   # loop time against the workgroup's tile count (bid -> key block as the kernel's grid order)
+    nxb = S // 256
+    hg = int(os.environ.get("HG", "4"))   # QA_DKV_HG of the build (0: longest-first over all heads)
+    bid = np.arange(nwg)
+    j = bid >> 3
+    if hg > 0 and (bh // 8) % hg == 0:
+        r = (j % (hg * nxb)) // hg
+    else:
+        r = j // (bh // 8)
+    ntile = S // 32 - 8 * r
+    A = np.vstack([np.ones(nwg), ntile]).T
+    coef = np.linalg.lstsq(A, loop, rcond=None)[0]
+    print(f"  tile loop ~ {coef[0]:.1f} us + {coef[1]:.3f} us per tile (fit over {nwg} workgroups); "
+          f"per-tile time by length: " + " ".join(f"{n}:{np.median(loop[ntile == n]) / n:.2f}" for n in (8, 32, 64, 96, 128)))
 order = np.argsort(us[:, 0])
 starts = us[order, 0]
 print("  start-time histogram (us):", np.histogram(starts, bins=8)[0].tolist(),
