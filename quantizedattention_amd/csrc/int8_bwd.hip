@@ -1151,9 +1151,6 @@ static void launch_dqw_c(const void* ds8, const void* sds, const void* k_bf, con
                      (const _Float16*)sk, (_Float16*)dq, (int)bh, (int)sqt, (int)skt, group, sms);
 }
 
-#ifndef QA_CAUSAL_DKV_CHUNK
-#define QA_CAUSAL_DKV_CHUNK 1
-#endif
 // which: bit mask 1 = dV kernel, 4 = dK kernel, 8 = fused dK+dV kernel, 2 = dQ kernel,
 // 16 = fused dK+dV kernel writing the dS workspace ws, 32 = dQ from the dS workspace.
 // bh = batch * query heads; the key/value side has bh / group heads of skt rows.
@@ -1167,27 +1164,7 @@ static void bwd_launch_d(int which, const void* dO_i8, const void* sdO, const vo
   const long bkv = bh / group, ny = group * sqt;
   char* ds8 = (char*)ws;
   char* sds = ws ? ds8 + bh * (sqt / 32) * (skt / 32) * 1024 : nullptr;
-  // Causal: the dK+dV pass in chunks of key/value heads, each writing its part of the one
-  // workspace, then one dQ pass over all heads.  A chunk's streamed query-side bytes stay in the MALL
-  // (32-head chunks 4 x 315-328 us against 1344 us in one launch), while the
-  // causal dQ pass, whose longest-first grid leaves a tail per launch, runs once.
-  const long nbh = (skt + BwdCfg<D, ROLE_DKV>::XROWS - 1) / BwdCfg<D, ROLE_DKV>::XROWS;   // blocks per head
-  const long kvc = QA_CAUSAL_DKV_CHUNK && causal ? std::max(1L, (512 + nbh - 1) / nbh) : bkv;
-  if ((which & 16) && kvc < bkv) {
-    const long nqt = sqt / 32, nkt = skt / 32;
-    auto at = [](const void* p_, long bytes) { return (const void*)((const char*)p_ + bytes); };
-    for (long k0 = 0; k0 < bkv; k0 += kvc) {
-      const long nkv = std::min(kvc, bkv - k0);
-      const long qr = k0 * ny, kr = k0 * skt;           // first query / key row of the chunk
-      const long rec = k0 * group * nqt * nkt;          // its first record
-      launch_bwd<D, ROLE_DKV, true>(causal, at(k_i8, kr * D), at(v_i8, kr * D), at(sk, kr / 32 * 2),
-                                    at(sv, kr / 32 * 2), at(q_i8, qr * D), at(dO_i8, qr * D),
-                                    at(q_bf, qr * D * 2), at(dO_bf, qr * D * 2), at(LD, qr * 8),
-                                    at(sq, qr / 32 * 2), at(sdO, qr / 32 * 2), nullptr,
-                                    (char*)dk + kr * D * 2, (char*)dv + kr * D * 2, nkv, skt, ny, 1, sqt,
-                                    qks, sms, st, ds8 + rec * 1024, sds + rec * 4);
-    }
-  } else if (which & 16)
+  if (which & 16)
     launch_bwd<D, ROLE_DKV, true>(causal, k_i8, v_i8, sk, sv, q_i8, dO_i8, q_bf, dO_bf, LD, sq, sdO,
                                   nullptr, dk, dv, bkv, skt, ny, 1, sqt, qks, sms, st, ds8, sds);
   if (which & 32) {
