@@ -220,6 +220,17 @@ int qattn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void*
 int qattn_bf16_fwd_ex(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
                       long sq, long sk, int group, int causal, int head_dim, float qks, void* stream);
 
+/* Size in bytes of the V-suffix workspace of qattn_bf16_fwd_ws_ex: bh_kv*(sk/32+1)*head_dim*4. */
+long qattn_bf16_fwd_ws_bytes(long bh_kv, long sk, int head_dim);
+/* qattn_bf16_fwd_ex with a scratch workspace (16-byte aligned, qattn_bf16_fwd_ws_bytes(bh / group,
+ * sk, head_dim) bytes) for the causal case: the per-head suffix sums of V are written there first and
+ * replace the fully masked sub-tiles past each 32-query block's diagonal (whose P is one constant,
+ * attention_bf16.py:222-285), so the causal forward streams half the key tiles.  Same outputs as
+ * qattn_bf16_fwd_ex up to fp32 summation order.  Non-causal calls, and ws == NULL, ignore it. */
+int qattn_bf16_fwd_ws_ex(const void* q, const void* k, const void* v, void* out, void* lse, long bh,
+                         long sq, long sk, int group, int causal, int head_dim, float qks, void* ws,
+                         void* stream);
+
 /* Backward prologue, one pass: dO f32 -> dO_bf bf16 [rows, D] and LD f32x2 [rows] =
  * {lse[row], D = rowsum(dO*O)} (attention_bf16.py:416, computed once per row instead of per tile). */
 int qattn_bf16_bwd_prep(const void* dO, const void* O, const void* lse, void* dO_bf, void* LD, long bh,

@@ -54,6 +54,9 @@ SIGNATURES = {
     "qattn_int8_bwd_dq": [_vp] * 11 + [_c_long, _c_long, _c_int, _c_float, _c_float, _vp],
     "qattn_bf16_fwd": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_long, _c_long, _c_int, _c_int, _c_float, _vp],
     "qattn_bf16_fwd_ex": [_vp] * 5 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float, _vp],
+    "qattn_bf16_fwd_ws_bytes": [_c_long, _c_long, _c_int],
+    "qattn_bf16_fwd_ws_ex": [_vp] * 5 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
+                                          _vp, _vp],
     "qattn_bf16_bwd_ex": [_vp] * 10 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                         _c_float, _vp],
     "qattn_bf16_bwd_ws_bytes": [_c_long, _c_long, _c_long],
@@ -94,6 +97,7 @@ DEV_SIGNATURES = {
 
 # return types other than the int status code
 RESTYPES = {"qattn_int8_bwd_ws_bytes": ctypes.c_long, "qattn_bf16_bwd_ws_bytes": ctypes.c_long,
+            "qattn_bf16_fwd_ws_bytes": ctypes.c_long,
             "qattn_bwd_ws_cap": ctypes.c_long}
 
 _lib = None

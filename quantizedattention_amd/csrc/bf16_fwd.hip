@@ -20,6 +20,14 @@
 // V read column-wise with ds_read_b64_tr_b16.  One 16-key sub-tile == one k-step of the
 // 32x32x16 PV MFMA.  Software pipeline: the QK^T MFMAs of tile t+1 are issued before the
 // softmax of tile t.
+//
+// Causal with a V-suffix workspace (qattn_bf16_fwd_ws_ex): past a wave's diagonal tile every score
+// is the fill value -126, the running max can no longer move (the diagonal tile already holds the
+// fill at key == query, so m >= bf16(-126 qks)) and the beta rule cannot fire (its threshold is
+// >= bf16(-126 qks) - 1e-3 > -126), so every masked sub-tile adds the same P = p to each key:
+// O += p * sum_{k >= K0} V[k], l += p * (Sk - K0).  bf16_vsuffix_* compute sum_{k >= 32 b} V[k]
+// once per key/value head; the tile loop stops at the workgroup's last diagonal tile and a wave
+// skips the tiles past its own, replacing the masked half of the P.V MFMAs by one FMA per output.
 #include <type_traits>
 
 #include "common.h"
@@ -99,10 +107,61 @@ QA_DEVICE unsigned rne2(float a, float b, float& ra, float& rb) {
 }
 QA_DEVICE float rne1(float a) { return __uint_as_float(pk_bf16(a, a) & 0xffff0000u); }
 
-template <int D, bool CAUSAL>
+// Per key/value head, per 32-key tile b: T[b][d] = sum of V[32b .. 32b+31][d] (fp32).  256
+// threads: 16-B column chunks x row groups, reduced through LDS.
+template <int D>
+__global__ __launch_bounds__(256) void bf16_vsuffix_tiles(const __bf16* __restrict__ v,
+                                                          float* __restrict__ ws, int nt) {
+  constexpr int NC = D / 8, RG = 256 / NC;   // column chunks, row groups
+  __shared__ float part[RG][D];
+  const int bt = blockIdx.x, hkv = bt / nt, t = bt % nt;
+  const int c = threadIdx.x % NC, rg = threadIdx.x / NC;
+  const __bf16* src = v + ((long)hkv * nt * 32 + (long)t * 32) * D + 8 * c;
+  float a[8] = {};
+  for (int r = rg; r < 32; r += RG) {
+    const v8bf x = *reinterpret_cast<const v8bf*>(src + (long)r * D);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += (float)x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[rg][8 * c + j] = a[j];
+  __syncthreads();
+  if (threadIdx.x < D) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < RG; ++g) s += part[g][threadIdx.x];
+    ws[((long)hkv * (nt + 1) + t) * D + threadIdx.x] = s;
+  }
+}
+
+// In place, per key/value head: ws[b][d] = sum_{b' >= b} T[b'][d], ws[nt][d] = 0.  1024 threads =
+// NG groups of D columns; group g scans its run of tiles on top of the totals of the groups after it.
+template <int D>
+__global__ __launch_bounds__(1024) void bf16_vsuffix_scan(float* __restrict__ ws, int nt) {
+  constexpr int NG = 1024 / D;
+  __shared__ float tot[NG][D];
+  const int d = threadIdx.x % D, g = threadIdx.x / D;
+  const int per = (nt + NG - 1) / NG, b0 = min(g * per, nt), b1 = min(b0 + per, nt);
+  float* w = ws + (long)blockIdx.x * (nt + 1) * D + d;
+  float s = 0.f;
+  for (int b = b0; b < b1; ++b) s += w[(long)b * D];
+  tot[g][d] = s;
+  __syncthreads();
+  float acc = 0.f;
+  for (int g2 = NG - 1; g2 > g; --g2) acc += tot[g2][d];
+  for (int b = b1 - 1; b >= b0; --b) {
+    acc += w[(long)b * D];
+    w[(long)b * D] = acc;
+  }
+  if (g == 0) w[(long)nt * D] = 0.f;
+}
+
+template <int D, bool CAUSAL, bool SFX>
 __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
     const _Float16* __restrict__ q, const _Float16* __restrict__ k, const __bf16* __restrict__ v,
-    float* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks) {
+    float* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks,
+    const float* __restrict__ vsuf) {
+  static_assert(!SFX || CAUSAL, "the V-suffix path is causal only");
   using C = Bf16FwdCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nq = (Sq + C::QROWS - 1) / C::QROWS;
@@ -117,13 +176,15 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
   const int qidx = q0 + c32;                     // this lane's query row
   const float thr_eps = 0.00099945068359375f;    // bf16(1e-3): eager `bf16 - 1e-3` rounds the scalar (bf16:248)
   const int nt = Sk / C::KT;
+  // SFX: the workgroup's last diagonal tile ends the loop (tiles past it are masked for every wave)
+  const int nte = SFX ? min(nt, (qt * C::QROWS + C::QROWS) / C::KT) : nt;
 
   Bf16Dma<D> dma;
   // grouped-query attention: query head bh reads key/value head bh / G
   dma.init(wave, lane, Sk, k + (long)(bh / G) * Sk * D, v + (long)(bh / G) * Sk * D);
   const unsigned smem_lds = lds_addr(smem);
 #pragma unroll
-  for (int i = 0; i < C::NSLOT - 1; ++i) dma.issue(smem_lds + i * C::SLOT, min(i, nt - 1));
+  for (int i = 0; i < C::NSLOT - 1; ++i) dma.issue(smem_lds + i * C::SLOT, min(i, nte - 1));
 
   v8h qf[C::NKS];
   {
@@ -276,8 +337,8 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
   // tile t lives in slot t & 3; at tile t the slot (t+1)&3 holds tile min(t+1, nt-1)
   auto step = [&](auto SLc, auto NXc, auto FRc, int t) {
     ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
-    dma.issue(smem_lds + decltype(FRc)::value * C::SLOT, min(t + 3, nt - 1));
-    {
+    dma.issue(smem_lds + decltype(FRc)::value * C::SLOT, min(t + 3, nte - 1));
+    if (!(SFX && masked(t, 0))) {   // SFX: a tile past the wave's diagonal is in the suffix
       // (a tile masked for the whole wave needs no S: its QK^T MFMAs are skipped)
       v16f nacc = v16f{};
       if (!masked(t + 1, 0)) nacc = qk(NXc);
@@ -291,11 +352,40 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
       acc = nacc;
     }
   };
-  for (int t = 0; t < nt; t += 4) {
+  for (int t = 0; t < nte; t += 4) {
     step(I0{}, I1{}, I3{}, t);
-    if (t + 1 < nt) step(I1{}, I2{}, I0{}, t + 1);
-    if (t + 2 < nt) step(I2{}, I3{}, I1{}, t + 2);
-    if (t + 3 < nt) step(I3{}, I0{}, I2{}, t + 3);
+    if (t + 1 < nte) step(I1{}, I2{}, I0{}, t + 1);
+    if (t + 2 < nte) step(I2{}, I3{}, I1{}, t + 2);
+    if (t + 3 < nte) step(I3{}, I0{}, I2{}, t + 3);
+  }
+  if constexpr (SFX) {
+    // the masked keys K0 .. Sk-1 of this wave, all at once (see the header)
+    const int K0 = q0 + 32;
+    if (K0 < Sk) {
+      const float cfill = rne1(-126.0f * qks);
+      const float nm = __builtin_amdgcn_fmed3f(m, cfill, inf);   // == m (kept for the general rule)
+      const float r = rne1(exp2_f32(rne1(m - nm)));
+      if (__ballot(r != 1.0f)) {
+#pragma unroll
+        for (int b = 0; b < C::NDB; ++b)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[b][i] = o[b][i] * r;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lacc[i] = lacc[i] * r;
+      }
+      m = nm;
+      const float p = rne1(exp2_f32(rne1(cfill - m)));
+      const float* vs = vsuf + ((long)(bh / G) * (nt + 1) + K0 / C::KT) * D + 4 * h;
+#pragma unroll
+      for (int b = 0; b < C::NDB; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const v4f x = *reinterpret_cast<const v4f*>(vs + 32 * b + 8 * g);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[b][4 * g + j] += p * x[j];
+        }
+      lacc[0] += p * (float)(Sk - K0);
+    }
   }
   vmcnt_wait_all();
   __syncthreads();   // the ring becomes the output staging area
@@ -310,30 +400,54 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
 
 using namespace qattn;
 
-extern "C" int qattn_bf16_fwd_ex(const void* q, const void* k, const void* v, void* out, void* lse,
-                                 long bh, long sq, long sk, int group, int causal, int head_dim,
-                                 float qks, void* stream) {
+extern "C" long qattn_bf16_fwd_ws_bytes(long bh_kv, long sk, int head_dim) {
+  return bh_kv * (sk / 32 + 1) * head_dim * 4;
+}
+
+extern "C" int qattn_bf16_fwd_ws_ex(const void* q, const void* k, const void* v, void* out, void* lse,
+                                    long bh, long sq, long sk, int group, int causal, int head_dim,
+                                    float qks, void* ws, void* stream) {
   if (sq % 32 != 0 || sk % 32 != 0 || group < 1 || bh % group != 0 ||
       (head_dim != 64 && head_dim != 128))
     return 1;
   if (bh == 0 || sq == 0) return 0;
+  if (ws != nullptr && (reinterpret_cast<uintptr_t>(ws) & 15) != 0) return 1;
   hipStream_t st = (hipStream_t)stream;
-#define QA_LAUNCH(Dv, CV)                                                                        \
+  const int nt = (int)(sk / 32);
+  const bool sfx = causal && ws != nullptr && nt > 0;
+  if (sfx) {   // the per-head V suffix sums the causal loop stops short of
+    const long hkv = bh / group;
+    if (head_dim == 128) {
+      hipLaunchKernelGGL(bf16_vsuffix_tiles<128>, dim3((unsigned)(hkv * nt)), dim3(256), 0, st, (const __bf16*)v, (float*)ws, nt);
+      hipLaunchKernelGGL(bf16_vsuffix_scan<128>, dim3((unsigned)hkv), dim3(1024), 0, st, (float*)ws, nt);
+    } else {
+      hipLaunchKernelGGL(bf16_vsuffix_tiles<64>, dim3((unsigned)(hkv * nt)), dim3(256), 0, st, (const __bf16*)v, (float*)ws, nt);
+      hipLaunchKernelGGL(bf16_vsuffix_scan<64>, dim3((unsigned)hkv), dim3(1024), 0, st, (float*)ws, nt);
+    }
+  }
+#define QA_LAUNCH(Dv, CV, SV)                                                                    \
   {                                                                                              \
     using C = Bf16FwdCfg<Dv>;                                                                    \
     const int nq = (int)((sq + C::QROWS - 1) / C::QROWS);                                        \
-    { static int granted_ = 0; lds_grant((const void*)bf16_fwd_kernel<Dv, CV>, C::LDS, granted_); }                     \
-    hipLaunchKernelGGL((bf16_fwd_kernel<Dv, CV>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), \
+    { static int granted_ = 0; lds_grant((const void*)bf16_fwd_kernel<Dv, CV, SV>, C::LDS, granted_); } \
+    hipLaunchKernelGGL((bf16_fwd_kernel<Dv, CV, SV>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), \
                        C::LDS, st, (const _Float16*)q, (const _Float16*)k, (const __bf16*)v,     \
-                       (float*)out, (float*)lse, (int)bh, (int)sq, (int)sk, group, qks);         \
+                       (float*)out, (float*)lse, (int)bh, (int)sq, (int)sk, group, qks,          \
+                       (const float*)ws);                                                        \
   }
   if (head_dim == 128) {
-    if (causal) QA_LAUNCH(128, true) else QA_LAUNCH(128, false)
+    if (sfx) QA_LAUNCH(128, true, true) else if (causal) QA_LAUNCH(128, true, false) else QA_LAUNCH(128, false, false)
   } else {
-    if (causal) QA_LAUNCH(64, true) else QA_LAUNCH(64, false)
+    if (sfx) QA_LAUNCH(64, true, true) else if (causal) QA_LAUNCH(64, true, false) else QA_LAUNCH(64, false, false)
   }
 #undef QA_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int qattn_bf16_fwd_ex(const void* q, const void* k, const void* v, void* out, void* lse,
+                                 long bh, long sq, long sk, int group, int causal, int head_dim,
+                                 float qks, void* stream) {
+  return qattn_bf16_fwd_ws_ex(q, k, v, out, lse, bh, sq, sk, group, causal, head_dim, qks, nullptr, stream);
 }
 
 extern "C" int qattn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void* lse, long bh,

@@ -115,6 +115,41 @@ def test_bf16_gqa_fwd_bwd(lib, hq, hkv, sq, sk, causal):
         assert _rel(a.cpu(), b) <= 1e-2, (name, _rel(a.cpu(), b))
 
 
+@pytest.mark.parametrize("hq,hkv,sq,sk,d", [(4, 4, 1024, 1024, 128), (4, 2, 512, 1024, 64),
+                                          (2, 1, 384, 256, 128), (2, 2, 1056, 1056, 64)])
+def test_bf16_fwd_causal_vsuffix_matches_tile_loop(lib, hq, hkv, sq, sk, d):
+    """The causal V-suffix path (qattn_bf16_fwd_ws_ex) against the full masked tile loop
+    (qattn_bf16_fwd_ex, no workspace): the masked sub-tiles' constant P times the suffix sum of V
+    equals their P.V MFMAs up to fp32 summation order; GQA, Sq != Sk, ragged workgroups
+    (1056 = 8 x 128 + 32).  The tile loop adds 16 p per sub-tile to l (and p.V to O) one sub-tile at
+    a time, as the reference does (bf16:279-285), and those fp32 additions of a small term to a larger
+    one round the same way each time: measured 2.2e-5 on O and 1.0e-5 on lse at 1024 keys, in the
+    first rows (the longest masked suffix), falling off with the row.  Bound: 1e-4 (the oracle
+    tolerance is 5e-3)."""
+    import math
+    from quantizedattention_amd import _lib
+    g = torch.Generator().manual_seed(41)
+    q = torch.randn((1, hq, sq, d), generator=g).half().cuda()
+    k = torch.randn((1, hkv, sk, d), generator=g).half().cuda()
+    v = torch.randn((1, hkv, sk, d), generator=g).bfloat16().cuda()
+    qks = float(torch.tensor(1.0 / math.sqrt(d) * 1.44269504, dtype=torch.float32))
+    outs = []
+    for use_ws in (False, True):
+        O = torch.full((hq, sq, d), float("nan"), device="cuda")
+        lse = torch.full((hq, sq), float("nan"), device="cuda")
+        ws = torch.full((lib.qattn_bf16_fwd_ws_bytes(hkv, sk, d) // 4,), float("nan"), device="cuda")
+        fn = "qattn_bf16_fwd_ws_ex" if use_ws else "qattn_bf16_fwd_ex"
+        args = (_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(O), _lib.ptr(lse), hq, sq, sk, hq // hkv,
+                1, d, qks) + ((_lib.ptr(ws),) if use_ws else ()) + (_lib.stream_of(q),)
+        _lib.call(fn, *args)
+        outs.append((O, lse))
+    torch.cuda.synchronize()
+    (O0, l0), (O1, l1) = outs
+    assert torch.isfinite(O1).all() and torch.isfinite(l1).all()
+    assert (O1 - O0).abs().max().item() <= 1e-4
+    assert (l1 - l0).abs().max().item() <= 1e-4
+
+
 @pytest.mark.parametrize("hq,hkv,sq,sk,d,causal", [
     (2, 2, 256, 256, 128, False), (2, 2, 256, 256, 128, True), (4, 2, 160, 224, 128, False),
     (4, 1, 96, 192, 128, True), (2, 2, 192, 320, 64, False), (3, 3, 128, 128, 64, True),
