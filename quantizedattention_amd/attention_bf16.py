@@ -70,11 +70,11 @@ def helion_atten_bf16_fwd_training(
     lse = torch.empty((B * H, S), dtype=torch.float32, device=q.device)
     qks = _f32(1.0 / math.sqrt(D) * 1.44269504)
     # grouped-query attention (SURVEY §8f N2 extension): query head h reads k/v head h // (H / Hkv);
-    # causal: the per-head V suffix sums stand in for the fully masked key tiles (include/qattn.h)
+    # causal: the per-head V suffix sums stand in for the fully masked key tiles (include/qattn.h);
+    # without room for them the kernel runs the whole masked tile loop (same results)
     ws = None
     if causal and Sk > 0:
-        nbytes = _lib.load().qattn_bf16_fwd_ws_bytes(B * k.shape[1], Sk, D)
-        ws = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
+        ws = _lib.try_workspace(_lib.load().qattn_bf16_fwd_ws_bytes(B * k.shape[1], Sk, D), q.device)
     _lib.call("qattn_bf16_fwd_ws_ex", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(O), _lib.ptr(lse),
               B * H, S, Sk, H // k.shape[1], int(bool(causal)), D, qks, _lib.ptr(ws), _lib.stream_of(q))
     return O, lse

@@ -264,12 +264,12 @@ std::tuple<Tensor, Tensor> bf16_fwd(const Tensor& q_in, const Tensor& k_in, cons
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3), Sk = k.size(2);
   Tensor O = empty({B, H, S, D}, at::kFloat, q), lse = empty({B * H, S}, at::kFloat, q);
   if (O.numel() == 0 || k.numel() == 0) return {O.zero_(), lse.zero_()};
-  // causal: the per-head V suffix sums stand in for the fully masked key tiles (include/qattn.h)
+  // causal: the per-head V suffix sums stand in for the fully masked key tiles (include/qattn.h);
+  // without room for them the kernel runs the whole masked tile loop (same results)
   Tensor ws;
-  if (causal)
-    ws = empty({qattn_bf16_fwd_ws_bytes(B * k.size(1), Sk, (int)D) / 4}, at::kFloat, q);
+  if (causal) ws = try_empty(qattn_bf16_fwd_ws_bytes(B * k.size(1), Sk, (int)D), q);
   call(qattn_bf16_fwd_ws_ex(P(q), P(k), P(v), P(O), P(lse), B * H, S, Sk, (int)(H / k.size(1)),
-                            causal ? 1 : 0, (int)D, qk_scale(D), causal ? P(ws) : nullptr, c.stream),
+                            causal ? 1 : 0, (int)D, qk_scale(D), P(ws), c.stream),
        "bf16 forward");
   return {O, lse};
 }
