@@ -235,6 +235,19 @@ def other_configs(n):
     out["cfg2_bf16_fwd_bwd"] = {"shape": [B, H, S, D], "ms": t, "TFLOPs": flop / (t * 1e-3) / 1e12,
                                 "frac_of_bf16_peak": flop / (t * 1e-3) / PEAK_BF16,
                                 "fwd_ms": tf, "fwd_TFLOPs": 4 * B * H * S * S * D / (tf * 1e-3) / 1e12}
+
+    # config 2 causal (causal=True secondary, credited half the flops); the forward
+    # replaces the masked keys past each diagonal by per-head V suffix sums (bf16_fwd.hip)
+    def bf16_causal_step():
+        O, lse = helion_atten_bf16_fwd_training(q, k, v, True)
+        helion_flash_atten_2_algo_4_bwd(q, k, v, O, lse, True, dO)
+    t = event_time(bf16_causal_step, n)
+    tf = event_time(lambda: helion_atten_bf16_fwd_training(q, k, v, True), n)
+    out["cfg2_bf16_causal_fwd_bwd"] = {"shape": [B, H, S, D], "ms": t,
+                                       "TFLOPs": 0.5 * flop / (t * 1e-3) / 1e12,
+                                       "frac_of_bf16_peak": 0.5 * flop / (t * 1e-3) / PEAK_BF16,
+                                       "fwd_ms": tf,
+                                       "fwd_TFLOPs": 2 * B * H * S * S * D / (tf * 1e-3) / 1e12}
     del q, k, v, dO
     # config 3 causal (SURVEY §8f N2 extension): int8 fwd+bwd, credited 7·BH·S²·D (half the scores)
     B, H, S, D = 4, 32, 4096, 128
