@@ -1,7 +1,8 @@
 """Build libqattn.so (all HIP kernels + the C-ABI) in-tree for gfx950.
 
 Plain hipcc, no torch headers: the library is a C-ABI boundary (include/qattn.h) that any host
-(ctypes here) binds.  Objects are rebuilt when a source or header is newer than the object.
+(ctypes here) binds.  Objects are rebuilt when a source, a header or this file (the flags) is newer
+than the object.
 """
 from __future__ import annotations
 
@@ -39,6 +40,11 @@ FILE_FLAGS = {
     # loop iteration for the (rare) rescale; the VGPR form keeps them in VGPRs and moves the Q
     # fragments to AGPRs instead (287 instead of 534 vector instructions per 64 keys).
     "jvp_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+    # The int8 forward under the max-ilp machine scheduler: same code, ordered for latency; no spill
+    # in any instantiation, bit-identical outputs, -1.2 % non-causal and -1.5 to -3 % causal at
+    # config 3 (profiles/r05_int8_fwd_sched_ab.log).  (iterative-ilp spills here; max-ilp spills the
+    # dK+dV kernel, and the bf16 forward does not move under either.)
+    "int8_attn_fwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
 }
 
 
@@ -112,7 +118,8 @@ def build_torch_ops(verbose: bool = True) -> Path:
 
 def _build_lib(srcs, lib, prefix: str, verbose: bool, jobs: int) -> None:
     BUILD.mkdir(exist_ok=True)
-    headers = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
+    # (this file too: it holds the compile flags)
+    headers = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h")) + [Path(__file__)]
     hdr_mtime = max((h.stat().st_mtime for h in headers), default=0.0)
     todo = []
     objs = []
