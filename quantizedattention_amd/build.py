@@ -39,12 +39,16 @@ FILE_FLAGS = {
     # by default hipcc gives the MFMAs AGPR accumulators and copies all 128 of them to VGPRs at every
     # loop iteration for the (rare) rescale; the VGPR form keeps them in VGPRs and moves the Q
     # fragments to AGPRs instead (287 instead of 534 vector instructions per 64 keys).
-    "jvp_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+    "jvp_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     # The int8 forward under the max-ilp machine scheduler: same code, ordered for latency; no spill
     # in any instantiation, bit-identical outputs, -1.2 % non-causal and -1.5 to -3 % causal at
     # config 3 (profiles/r05_int8_fwd_sched_ab.log).  (iterative-ilp spills here; max-ilp spills the
     # dK+dV kernel, and the bf16 forward does not move under either.)
     "int8_attn_fwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    # the same scheduler for the JVP forward (config 5: 0.270-0.272 against 0.276 ms) and the MX-FP4
+    # forward (536-544 against 545-559 us); the bf16 backward is slower under it (3.85 against 3.79-3.83
+    # ms) and keeps the default (profiles/r05_int8_fwd_sched_ab.log)
+    "mxfp4_attn.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
 }
 
 
