@@ -28,6 +28,18 @@
 extern "C" {
 #endif
 
+/* ---------------------------------------------------------------- versioning
+ * QATTN_ABI_VERSION counts incompatible changes of the entries below (a changed argument list under
+ * an old name; INTEGRATION.md §"ABI versions" lists them).  A host compiled against this header
+ * checks qattn_abi_version() == QATTN_ABI_VERSION after loading the library and refuses to call it
+ * otherwise: a library of another version would read its arguments with another meaning.
+ * qattn_source_hash() is the sha256 (hex) of the kernel sources and compile flags the library was
+ * built from (quantizedattention_amd/_srchash.py); the Python binding refuses a library whose hash
+ * differs from the sources beside it (a stale prebuilt library). */
+#define QATTN_ABI_VERSION 6
+int qattn_abi_version(void);
+const char* qattn_source_hash(void);
+
 /* ---------------------------------------------------------------- int8 path (attention_int8.py) */
 
 /* Per-32-row block quantiser (attention_int8.py:178-186 q, 188-195 k, 241-247 v).

@@ -22,6 +22,8 @@ _vp = ctypes.c_void_p
 
 # name -> argtypes (restype is always int status: 0 ok, 1 invalid argument, 2 launch failure)
 SIGNATURES = {
+    "qattn_abi_version": [],
+    "qattn_source_hash": [],
     "qattn_int8_quant": [_vp, _vp, _vp, _vp, _vp, _c_long, _c_int, _c_int, _vp],
     "qattn_int8_quant_img": [_vp] * 6 + [_c_long, _c_int, _c_int, _vp],
     "qattn_int8_dequant": [_vp, _vp, _vp, _c_long, _c_int, _vp],
@@ -96,9 +98,13 @@ DEV_SIGNATURES = {
 }
 
 # return types other than the int status code
-RESTYPES = {"qattn_int8_bwd_ws_bytes": ctypes.c_long, "qattn_bf16_bwd_ws_bytes": ctypes.c_long,
+RESTYPES = {"qattn_abi_version": ctypes.c_int, "qattn_source_hash": ctypes.c_char_p,
+            "qattn_int8_bwd_ws_bytes": ctypes.c_long, "qattn_bf16_bwd_ws_bytes": ctypes.c_long,
             "qattn_bf16_fwd_ws_bytes": ctypes.c_long,
             "qattn_bwd_ws_cap": ctypes.c_long}
+
+# include/qattn.h QATTN_ABI_VERSION: the argument lists SIGNATURES describes
+ABI_VERSION = 6
 
 _lib = None
 _dev = None
@@ -125,6 +131,17 @@ def load(path: os.PathLike | None = None) -> ctypes.CDLL:
             raise QAttnError(f"{p} does not export {name} (stale build? rebuild it)")
         fn.argtypes = argtypes
         fn.restype = RESTYPES.get(name, ctypes.c_int)
+    if lib.qattn_abi_version() != ABI_VERSION:
+        raise QAttnError(f"{p}: C ABI version {lib.qattn_abi_version()}, this binding speaks "
+                         f"{ABI_VERSION} (include/qattn.h QATTN_ABI_VERSION); rebuild the library")
+    from . import _srchash
+    if _srchash.available() and os.environ.get("QATTN_LIB") is None:
+        built = lib.qattn_source_hash().decode()
+        want = _srchash.library_hash()
+        if built != want:
+            raise QAttnError(
+                f"{p} is stale: built from sources/flags {built[:12]}, the tree holds {want[:12]} "
+                "(rebuild it with `python -m quantizedattention_amd.build`)")
     _lib = lib
     return lib
 

@@ -60,9 +60,38 @@ def _compile(src: Path, obj: Path) -> str:
     return src.name
 
 
+STAMP = BUILD / "source_hash"
+VERSION_SRC = BUILD / "qattn_version.cpp"
+
+
+def _version_object(digest: str, verbose: bool) -> Path:
+    """The generated qattn_abi_version() / qattn_source_hash() of include/qattn.h."""
+    src = (f'#include "qattn.h"\n'
+           f'extern "C" int qattn_abi_version(void) {{ return QATTN_ABI_VERSION; }}\n'
+           f'extern "C" const char* qattn_source_hash(void) {{ return "{digest}"; }}\n')
+    obj = BUILD / "qattn_version.o"
+    if not obj.exists() or not VERSION_SRC.exists() or VERSION_SRC.read_text() != src:
+        VERSION_SRC.write_text(src)
+        cmd = [HIPCC, "-O2", "-std=c++17", "-fPIC", f"-I{INCLUDE}", "-c", str(VERSION_SRC), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {VERSION_SRC.name}:\n{r.stderr}")
+        if verbose:
+            print(f"[qattn build] compiled {VERSION_SRC.name}", file=sys.stderr)
+    return obj
+
+
 def build(verbose: bool = True, jobs: int = 8) -> Path:
-    _build_lib(sorted(CSRC.glob("*.hip")), LIB, "", verbose, jobs)
-    _build_lib(sorted((CSRC / "dev").glob("*.hip")), DEV_LIB, "dev_", verbose, jobs)
+    from ._srchash import library_hash
+    BUILD.mkdir(exist_ok=True)
+    digest = library_hash()
+    # a change of sources or flags rebuilds every object, whatever the file times say (a tree copied
+    # to another machine may carry any mtimes)
+    force = not STAMP.exists() or STAMP.read_text().strip() != digest
+    ver = _version_object(digest, verbose)
+    _build_lib(sorted(CSRC.glob("*.hip")), LIB, "", verbose, jobs, force, extra=[ver])
+    _build_lib(sorted((CSRC / "dev").glob("*.hip")), DEV_LIB, "dev_", verbose, jobs, force)
+    STAMP.write_text(digest + "\n")
     build_torch_ops(verbose)
     build_c_host(verbose)
     return LIB
@@ -120,7 +149,8 @@ def build_torch_ops(verbose: bool = True) -> Path:
     return OPS_LIB
 
 
-def _build_lib(srcs, lib, prefix: str, verbose: bool, jobs: int) -> None:
+def _build_lib(srcs, lib, prefix: str, verbose: bool, jobs: int, force: bool = False,
+               extra=()) -> None:
     BUILD.mkdir(exist_ok=True)
     # (this file too: it holds the compile flags)
     headers = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h")) + [Path(__file__)]
@@ -130,8 +160,9 @@ def _build_lib(srcs, lib, prefix: str, verbose: bool, jobs: int) -> None:
     for s in srcs:
         o = BUILD / (prefix + s.stem + ".o")
         objs.append(o)
-        if not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr_mtime):
+        if force or not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr_mtime):
             todo.append((s, o))
+    objs += list(extra)
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             for name in ex.map(lambda so: _compile(*so), todo):

@@ -104,6 +104,12 @@ struct SmTile {
 #ifndef QA_FWD_ABL
 #define QA_FWD_ABL 0
 #endif
+#ifndef QA_FWD_DQ_SCALAR
+#define QA_FWD_DQ_SCALAR 0
+#endif
+#ifndef QA_FWD_S_SCALAR
+#define QA_FWD_S_SCALAR 0
+#endif
 // Diagnostic build only (-DQA_FWD_LIT_COUNT=1, tools/ab_time.py): counts the literal wave-tiles and
 // all wave-tiles (vector atomics by lane 0 of each wave).
 #ifndef QA_FWD_LIT_COUNT
@@ -396,12 +402,18 @@ QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
   };
   // O += (KMAG + X) * (sp * sv) for the tile's exact int32 X (one fused op per element)
   auto pv_dequant = [&](float cpv) {
-    // explicit v_pk_fma_f32 pairs (scalar v_fma_f32 measured 2-3 % slower)
+    // explicit v_pk_fma_f32 pairs (scalar v_fma_f32 measured 2-3 % slower);
+    // QA_FWD_DQ_SCALAR (A/B, needs -fno-slp-vectorize): the first that many d blocks scalar
     const v2f_ c2 = {cpv, cpv};
 #pragma unroll
     for (int b = 0; b < C::NDB; ++b)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
+        if (b < QA_FWD_DQ_SCALAR) {
+          o[b][r] = __builtin_fmaf(__int_as_float(pacc[b][r]), cpv, o[b][r]);
+          o[b][r + 1] = __builtin_fmaf(__int_as_float(pacc[b][r + 1]), cpv, o[b][r + 1]);
+          continue;
+        }
         const v2f_ a = {__int_as_float(pacc[b][r]), __int_as_float(pacc[b][r + 1])};
         const v2f_ y = __builtin_elementwise_fma(a, c2, v2f_{o[b][r], o[b][r + 1]});
         o[b][r] = y[0];
@@ -448,6 +460,12 @@ QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
     const float nb = -KMAG * c;
     const _Float16 rm = biased_to_f16(mx, c, nb);
     biased_to_f16x16(acc, c, nb, s2);
+#if QA_FWD_S_SCALAR > 0   // (A/B, needs -fno-slp-vectorize: the first pairs in scalar fp32)
+#pragma unroll
+    for (int j = 0; j < QA_FWD_S_SCALAR; ++j)
+      s2[j] = v2h{(_Float16)__builtin_fmaf(__int_as_float(acc[2 * j]), c, nb),
+                  (_Float16)__builtin_fmaf(__int_as_float(acc[2 * j + 1]), c, nb)};
+#endif
     const v2h rm2 = {rm, rm};
 #pragma unroll
     for (int j = 0; j < 8; ++j) st.d[j] = s2[j] - rm2;   // f16(S - rm)  (int8:211, 232-236)

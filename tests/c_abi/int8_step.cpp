@@ -51,6 +51,10 @@ int main(int argc, char** argv) {
   const long B = std::atol(argv[1]), H = std::atol(argv[2]), S = std::atol(argv[3]);
   const int D = std::atoi(argv[4]);
   const std::string dir = argv[5];
+  if (qattn_abi_version() != QATTN_ABI_VERSION) {   // a library built against another header
+    std::fprintf(stderr, "libqattn ABI %d, this host speaks %d\n", qattn_abi_version(), QATTN_ABI_VERSION);
+    return 1;
+  }
   const long N = B * H * S;
   const size_t f16b = (size_t)N * D * 2, i8b = (size_t)N * D, sb = (size_t)(N / 32) * 2;
   // the scales of attention_int8.py:151-153 (double products rounded to fp32, as the drop-in does)

@@ -23,7 +23,7 @@ def header_decls():
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
-    for m in re.finditer(r"\b(int|long)\s+(qattn_\w+)\s*\(([^)]*)\)\s*;", text):
+    for m in re.finditer(r"\b(int|long|const char\s*\*)\s*(qattn_\w+)\s*\(([^)]*)\)\s*;", text):
         params = [p.strip() for p in m.group(3).split(",") if p.strip() and p.strip() != "void"]
         decls[m.group(2)] = params
     return decls
@@ -31,8 +31,8 @@ def header_decls():
 
 def header_returns():
     text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
-    return {m.group(2): m.group(1)
-            for m in re.finditer(r"\b(int|long)\s+(qattn_\w+)\s*\(([^)]*)\)\s*;", text)}
+    return {m.group(2): re.sub(r"\s+", "", m.group(1))
+            for m in re.finditer(r"\b(int|long|const char\s*\*)\s*(qattn_\w+)\s*\(([^)]*)\)\s*;", text)}
 
 
 def test_header_parses():
@@ -75,7 +75,19 @@ def test_library_loads_and_types():
     from quantizedattention_amd import _lib
     lib = _lib.load()
     for name, ret in header_returns().items():
-        assert getattr(lib, name).restype is (ctypes.c_long if ret == "long" else ctypes.c_int), name
+        want = {"long": ctypes.c_long, "int": ctypes.c_int, "constchar*": ctypes.c_char_p}[ret]
+        assert getattr(lib, name).restype is want, name
+
+
+@pytest.mark.skipif(not LIB.exists(), reason="libqattn.so not built (run __graft_entry__.build())")
+def test_abi_version_and_source_hash():
+    """The library speaks the header's ABI version and was built from the sources in the tree
+    (_lib.load refuses it otherwise: a stale prebuilt library must not run)."""
+    from quantizedattention_amd import _lib, _srchash
+    lib = _lib.load()
+    m = re.search(r"#define\s+QATTN_ABI_VERSION\s+(\d+)", HEADER.read_text())
+    assert m and int(m.group(1)) == _lib.ABI_VERSION == lib.qattn_abi_version()
+    assert lib.qattn_source_hash().decode() == _srchash.library_hash()
 
 
 def test_int8_error_messages():
