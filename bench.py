@@ -535,6 +535,8 @@ def main():
         "without_gather": None if t_ng is None else {
             "value": flop_step / t_ng / 1e12, "ms_per_step": t_ng * 1e3,
             "gather_cost_ms": (t_i8 - t_ng) * 1e3},
+        # "bound": the roof the peak is taken from -- MFMA by arithmetic intensity (>> the ridge,
+        # DESIGN.md §3); what limits the kernel in practice is "limiter" below (from the counters)
         "roofline": {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": PEAK_I8 / 1e12,
                      "unit": "TFLOP/s", "frac": achieved * 1e12 / PEAK_I8, "traffic": None,
                      "launch_ms": kt[dom], "work_per_launch": per_call[dom],
@@ -554,6 +556,22 @@ def main():
                 # dispatch time); the peak above assumes 2.4 GHz
                 if tr.get("clock_GHz", {}).get(dom):
                     out["roofline"]["clock_GHz_profiled"] = tr["clock_GHz"][dom]
+                # SURVEY §8d "also report the VALU ceiling": the counters of the same PMC passes
+                # (tools/profile_summary.py).  mfma_util: matrix-pipe busy share; valu_busy: share of
+                # cycles a SIMD's vector issue is taken (SQ_ACTIVE_INST_VALU, MFMA issue included);
+                # mfma_ceiling_frac: the kernel's attainable fraction of the int8 peak from its own
+                # MFMA mix (its bf16 products run at half the int8 rate); limiter: the busier of the
+                # two issue resources, i.e. what bounds the kernel in practice
+                fwd_c = out["int8_fwd"].setdefault("attention_kernel_counters", {})
+                for key, obj in ((dom, out["roofline"]), ("int8_attn_fwd_kernel", fwd_c)):
+                    c = tr.get("counters", {}).get(key, {})
+                    for f in ("mfma_util", "valu_busy", "mfma_ceiling_frac", "vector_insts_per_mfma"):
+                        if f in c:
+                            obj[f] = c[f]
+                    if "clock_GHz" in c:
+                        obj["clock_GHz_profiled"] = c["clock_GHz"]
+                    if "mfma_util" in c and "valu_busy" in c:
+                        obj["limiter"] = "valu_issue" if c["valu_busy"] > c["mfma_util"] else "mfma"
             else:
                 out["roofline"]["traffic_note"] = "PMC traffic in profiles/ is from other sources: omitted"
         except Exception:

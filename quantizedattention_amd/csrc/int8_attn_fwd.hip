@@ -46,6 +46,7 @@
 // tiles) move O by 1.3e-2 .. 6e-2 from the reference (tools/pv_quant_study.py), past the 1e-2 bar.
 // (An f16 P.V form on f16(P_i8 sp) x f16(v_i8 sv) measured 10-15 % slower and was removed in round 5.)
 #include <climits>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -731,6 +732,14 @@ __global__ __launch_bounds__((64 * Int8FwdCfg<D>::WAVES), 2) void int8_attn_fwd_
   }
 }
 
+// Diagnostic switch (tests/test_gpu_fixup.py): QATTN_FWD_SKIP_FIXUP=1 leaves out the separate fixup
+// launches, so the marks of the waves the fast pass handed over stay in lse (FIX_LSE16) / ml
+// (FIX_M32) where a test can count them.  Read per call; never set in production.
+static bool skip_fixup() {
+  const char* e = std::getenv("QATTN_FWD_SKIP_FIXUP");
+  return e != nullptr && e[0] == '1';
+}
+
 template <int D, bool CAUSAL, bool QF>
 static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const void* sk,
                       const void* vt, const void* sv, void* out, void* lse, long bh, long sq_tok,
@@ -749,6 +758,7 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
                      (const int8_t*)vt, (const _Float16*)sv, (_Float16*)out, (_Float16*)lse, (int)bh,
                      (int)sq_tok, (int)sk_tok, group, qoff, qks, (const _Float16*)q16, (__bf16*)qbf);
   if constexpr (C::LIT_K > 0 && QA_FWD_DEFER && !INL) {   // the waves whose votes held: redone
+    if (skip_fixup()) return hipGetLastError() == hipSuccess ? 0 : 2;
     auto fixk = int8_attn_fwd_kernel<D, CAUSAL, false, false, true>;
     { static int granted_ = 0; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
     hipLaunchKernelGGL(fixk, dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds, st,
@@ -807,6 +817,7 @@ static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, 
                      (_Float16*)opart, (_Float16*)ml, (int)bh, (int)sq_tok, (int)sk_tok, group, ks, qks,
                      nullptr, nullptr);
   if constexpr (C::LIT_K > 0 && QA_FWD_DEFER) {   // the split rows whose first tile must be redone
+    if (skip_fixup()) return hipGetLastError() == hipSuccess ? 0 : 2;
     auto fixk = int8_attn_fwd_kernel<D, false, true, false, true>;
     { static int granted_ = 0; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
     hipLaunchKernelGGL(fixk, dim3((unsigned)(nq * bh), (unsigned)nsplit), dim3(64 * C::WAVES), lds, st,

@@ -76,7 +76,10 @@ def test_profile_tools_tell_grids_apart(tmp_path):
     name = "void qattn::int8_bwd_kernel<128, 3, false, true>(signed char const*)"
     assert key_of(name, 512) == "int8_bwd_dkdv_kernel<dK+dV, dS out>"
     assert key_of(name, 2048) == "int8_bwd_dkdv_kernel<dK+dV, dS out, one pass>"
-    assert key_of("void qattn::int8_attn_fwd_kernel<128, 1, false>(x)", 4096) == "int8_attn_fwd_kernel"
+    fwd = "void qattn::int8_attn_fwd_kernel<128, false, false, true, false, true>(signed char const*)"
+    assert key_of(fwd, 4096) == "int8_attn_fwd_kernel"
+    fwd = "void qattn::int8_attn_fwd_kernel<128, false, false, false, false, false>(signed char const*)"
+    assert key_of(fwd, 4096) == "int8_attn_fwd_kernel<q_i8 in>"
     assert workgroups({"Grid_Size_X": "262144", "Workgroup_Size_X": "512"}) == 512
     d = tmp_path / "trace"
     d.mkdir()

@@ -22,6 +22,8 @@ alone (heads are independent).  Tolerances are the ones DESIGN.md §4 states:
 import pytest
 import torch
 
+from conftest import INT8_BWD_REL
+
 from oracle import restate as R
 
 pytestmark = pytest.mark.gpu
@@ -102,7 +104,9 @@ def test_cfg3_int8_bwd_full_length_one_head(lib):
     rq, rk, rv = R.int8_bwd(sl(dO), qi[rows].cpu(), sq[blk].cpu(), kiT[:, rows].cpu(), None,
                             sk[blk].cpu(), vi[rows].cpu(), sv[blk].cpu(), sl(O), lse[rows].cpu())
     for name, a, r in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
-        assert _rel(sl(a), r) <= 0.05, (name, _rel(sl(a), r))
+        rel = _rel(sl(a), r)
+        print(f"RELL2 int8-bwd-vs-oracle {name} {rel:.5f}")
+        assert rel <= INT8_BWD_REL, (name, rel)
     tq, tk, tv = R.attention_grads_truth(sl(q), sl(k), sl(v), sl(dO), False)
     for name, a, t in (("dq", dq, tq), ("dk", dk, tk), ("dv", dv, tv)):
         assert _rel(sl(a), t) <= 0.15, (name, _rel(sl(a), t))

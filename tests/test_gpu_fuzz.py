@@ -12,6 +12,8 @@ lse within 2 fp16 steps; grads relL2 <= 0.05 vs the oracle; the cached (decoding
 import pytest
 import torch
 
+from conftest import INT8_BWD_REL
+
 from oracle import restate as R
 
 pytestmark = pytest.mark.gpu
@@ -80,7 +82,8 @@ def test_int8_fuzz(lib, i):
         a = a.float().cpu()
         assert torch.isfinite(a).all(), name
         rel = ((a - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
-        assert rel <= 0.05, (name, rel)
+        print(f"RELL2 int8-bwd-vs-oracle {name} {rel:.5f}")
+        assert rel <= INT8_BWD_REL, (name, rel)
     # the decoding layout on the same operands (non-causal, head_dim 128)
     if not causal and D == 128:
         from quantizedattention_amd.kv_cache import attention_int8_cached, quantize_kv

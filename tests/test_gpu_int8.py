@@ -8,6 +8,8 @@ Tolerances (stated here):
 import pytest
 import torch
 
+from conftest import INT8_BWD_REL
+
 from oracle import restate as R
 
 pytestmark = pytest.mark.gpu
@@ -103,7 +105,9 @@ def test_int8_bwd_matches_oracle(lib, shape):
                             O.cpu(), lse.cpu())
     for name, a, b in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
         assert a.dtype == torch.float16 and a.shape == shape
-        assert _rel(a.cpu(), b) <= 0.05, (name, _rel(a.cpu(), b))
+        rel = _rel(a.cpu(), b)
+        print(f"RELL2 int8-bwd-vs-oracle {name} {rel:.5f}")
+        assert rel <= INT8_BWD_REL, (name, rel)
     tq, tk, tv = R.attention_grads_truth(q, k, v, dO, False)
     for name, a, b in (("dq", dq, tq), ("dk", dk, tk), ("dv", dv, tv)):
         assert _rel(a.cpu(), b) <= 0.15, (name, _rel(a.cpu(), b))

@@ -11,6 +11,8 @@ reference has no such shapes): the oracle pins the documented semantics.
 import pytest
 import torch
 
+from conftest import INT8_BWD_REL
+
 from oracle import restate as R
 
 pytestmark = pytest.mark.gpu
@@ -81,7 +83,9 @@ def test_int8_bwd_gqa_causal(lib, shape, causal):
     assert dq.shape == (B, Hq, Sq, D) and dk.shape == (B, Hkv, Sk, D) and dv.shape == dk.shape
     for name, a, b in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
         assert torch.isfinite(a).all(), name
-        assert _rel(a.cpu(), b) <= 0.05, (name, _rel(a.cpu(), b))
+        rel = _rel(a.cpu(), b)
+        print(f"RELL2 int8-bwd-vs-oracle {name} {rel:.5f}")
+        assert rel <= INT8_BWD_REL, (name, rel)
 
 
 def test_int8_autograd_gqa_causal(lib):
@@ -102,7 +106,9 @@ def test_int8_autograd_gqa_causal(lib):
     rq, rk, rv = R.int8_bwd(dO, ref[2], ref[5], ref[3], km, ref[6], ref[4], ref[7], ref[0], ref[1],
                             causal=True)
     for name, a, b in (("dq", qc.grad, rq), ("dk", kc.grad, rk), ("dv", vc.grad, rv)):
-        assert _rel(a.cpu(), b) <= 0.05, (name, _rel(a.cpu(), b))
+        rel = _rel(a.cpu(), b)
+        print(f"RELL2 int8-bwd-vs-oracle {name} {rel:.5f}")
+        assert rel <= INT8_BWD_REL, (name, rel)
 
 
 @pytest.mark.parametrize("shape", SHAPES + [(1, 2, 2, 256, 512, 128), (2, 3, 3, 96, 96, 128)])

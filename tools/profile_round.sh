@@ -30,6 +30,9 @@ echo "mfma done"
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_I8 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_BF16 \
   --output-format csv -d $OUT/mops -o run -- python3 $R/tools/kernel_runner.py int8_all 2 > /dev/null 2>&1
 echo "mops done"
+timeout -s KILL 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+  --output-format csv -d $OUT/valu -o run -- python3 $R/tools/kernel_runner.py int8_all 2 > /dev/null 2>&1
+echo "valu done"
 cd $R
 python3 tools/profile_summary.py $OUT $TAG $OUT/profiles > $OUT/pmc_summary.txt
 cp $OUT/profiles/traffic_latest.json profiles/traffic_latest.json

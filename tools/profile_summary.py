@@ -28,8 +28,11 @@ PROF = os.path.join(ROOT, "profiles")
 BH, S = 4 * 32, 4096
 CHUNK = 32
 KEYS = {
-    "int8_attn_fwd_kernel": (r"int8_attn_fwd_kernel(<128, ?1, ?false>|ILi128ELi1ELb0E)", None),
-    "int8_attn_fwd_kernel<f16 P.V>": (r"int8_attn_fwd_kernel(<128, ?0, ?false>|ILi128ELi0ELb0E)", None),
+    # the q-fused forward with the inline fixup <D, CAUSAL, SPLIT, QF, FIX, INL> (the drop-ins' kernel)
+    "int8_attn_fwd_kernel": (r"int8_attn_fwd_kernel(<128,false,false,true,false,true>|"
+                             r"ILi128ELb0ELb0ELb1ELb0ELb1E)", None),
+    "int8_attn_fwd_kernel<q_i8 in>": (r"int8_attn_fwd_kernel(<128,false,false,false,false,false>|"
+                                      r"ILi128ELb0ELb0ELb0ELb0ELb0E)", None),
     "int8_bwd_dkdv_kernel<dK+dV>": (r"int8_bwd_kernel(<128, ?3, ?false, ?false>|ILi128ELi3ELb0ELb0E)", None),
     "int8_bwd_dq_kernel": (r"int8_bwd_kernel(<128, ?2|ILi128ELi2E)", None),
     "int8_bwd_dkdv_kernel<dK+dV, dS out>": (r"int8_bwd_kernel(<128, ?3, ?false, ?true>|ILi128ELi3ELb0ELb1E)",
@@ -40,6 +43,11 @@ KEYS = {
     "int8_bwd_dqw_kernel<one pass>": (r"int8_bwd_dqw_kernel(<128|ILi128E)", BH * S // 256),
 }
 SIMDS_PER_XCD = 32 * 4
+# credited MFMA work per launch (bench.py per_call) and the dense peaks (2.4 GHz spec)
+CREDIT = {"int8_attn_fwd_kernel": 4.0 * BH * S * S * 128, "int8_attn_fwd_kernel<q_i8 in>": 4.0 * BH * S * S * 128,
+          "int8_bwd_dkdv_kernel<dK+dV, dS out>": 8.0 * CHUNK * S * S * 128,
+          "int8_bwd_dqw_kernel": 2.0 * CHUNK * S * S * 128}
+PEAK_I8, PEAK_BF16 = 256 * 8192 * 2.4e9, 256 * 4096 * 2.4e9
 # GRBM_GUI_ACTIVE is summed over the 8 XCDs; SQ_VALU_MFMA_BUSY_CYCLES counts 32 busy SIMD-cycles per
 # 32x32 MFMA (i8 32x32x32 and f16/bf16 32x32x16 alike: 65536 / 32768 ops at 2048 / 1024 ops/clk/SIMD)
 XCDS = 8
@@ -95,6 +103,7 @@ def main():
     write = counters(os.path.join(src, "write"))
     mfma = counters(os.path.join(src, "mfma"))
     mops = counters(os.path.join(src, "mops")) if os.path.isdir(os.path.join(src, "mops")) else {}
+    valu = counters(os.path.join(src, "valu")) if os.path.isdir(os.path.join(src, "valu")) else {}
     out, traffic = {}, {}
     for k in KEYS:
         e = {}
@@ -119,6 +128,22 @@ def main():
             e.update(m)
             e["mfma_ops_executed"] = 512 * sum(m.get(c, 0.0) for c in (
                 "SQ_INSTS_VALU_MFMA_MOPS_I8", "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_INSTS_VALU_MFMA_MOPS_BF16"))
+            if k in CREDIT and e["mfma_ops_executed"] > 0:
+                # the MFMA ceiling of the kernel's own mix: its executed i8 and f16/bf16 work at the
+                # dense peaks, against the work it is credited with (bf16 runs at half the i8 rate)
+                t_peak = (512 * m.get("SQ_INSTS_VALU_MFMA_MOPS_I8", 0.0) / PEAK_I8 + 512 * (
+                    m.get("SQ_INSTS_VALU_MFMA_MOPS_F16", 0.0) + m.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0))
+                    / PEAK_BF16)
+                e["mfma_ceiling_frac"] = CREDIT[k] / t_peak / PEAK_I8
+        if k in valu and valu[k].get("GRBM_GUI_ACTIVE"):
+            m = valu[k]
+            cyc = m["GRBM_GUI_ACTIVE"] / XCDS
+            e["valu_pass"] = {c: v for c, v in m.items()}
+            # SQ_ACTIVE_INST_VALU: quad-cycles in which a wave issues VALU work (MFMAs included),
+            # summed over waves: per SIMD, the share of cycles its vector issue is taken
+            e["valu_busy"] = 4 * m.get("SQ_ACTIVE_INST_VALU", 0.0) / (cyc * SIMDS_PER_XCD * XCDS)
+            e["vector_insts_per_mfma"] = (m.get("SQ_INSTS_VALU", 0.0) - m.get("SQ_INSTS_MFMA", 0.0)) / max(
+                1.0, m.get("SQ_INSTS_MFMA", 0.0))
         if "FETCH_bytes_x2" in e and "WRITE_bytes" in e:
             traffic[k] = e["FETCH_bytes_x2"] + e["WRITE_bytes"]
             e["hbm_bytes_per_launch"] = traffic[k]
@@ -133,7 +158,10 @@ def main():
         # bench.py reports these only while the kernel sources hash to source_sha256
         json.dump({"tag": tag, "source_sha256": source_hash(), "shape": [4, 32, 4096, 128],
                    "traffic": traffic,
-                   "clock_GHz": {k: e["clock_GHz"] for k, e in out.items() if "clock_GHz" in e}},
+                   "clock_GHz": {k: e["clock_GHz"] for k, e in out.items() if "clock_GHz" in e},
+                   "counters": {k: {f: e[f] for f in ("mfma_util", "valu_busy", "mfma_ceiling_frac",
+                                                       "vector_insts_per_mfma", "clock_GHz") if f in e}
+                                for k, e in out.items()}},
                   f, indent=1)
     print(json.dumps(out, indent=1))
 
