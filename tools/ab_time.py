@@ -24,12 +24,6 @@ lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 
 
 def entry(name):
-    if name == "qattn_int8_attn_fwd_ex" and getattr(lib, "qattn_int8_attn_fwd_i8pv_ex", None) is not None:
-        name_sig, name = name, "qattn_int8_attn_fwd_i8pv_ex"   # a round-4 library (same arguments)
-        fn = getattr(lib, name)
-        fn.argtypes = SIGNATURES[name_sig]
-        fn.restype = ctypes.c_int
-        return fn
     fn = getattr(lib, name, None)
     if fn is not None:
         fn.argtypes = SIGNATURES[name]
