@@ -78,6 +78,13 @@ int qattn_int8_v_image(const void* v_i8, void* vt, long rows, int head_dim, void
  * (SageAttention smoothing; replaces the crashing `k.mean(0)` of attention_int8.py:24-25). */
 int qattn_kmean(const void* k, void* kmean, long bh, long seq, int head_dim, void* stream);
 
+/* qattn_kmean followed by qattn_int8_quant_img of the smoothed k, in one launch (attention_int8.py:
+ * 24-25 smoothing, 188-195 k quantiser): kmean f16 [bh, D], k_i8 i8 [bh*seq, D], sk f16
+ * [bh*seq/32] and (k_bf != NULL) the bf16 image bf16(k_i8) out, bit-identical with the two calls.
+ * seq % 32 == 0. */
+int qattn_int8_quant_k_smooth(const void* k, void* kmean, void* k_i8, void* sk, void* k_bf, long bh,
+                              long seq, int head_dim, void* stream);
+
 /* int8 SageAttention-3 forward, per (batch, head) (attention_int8.py:197-257; per-head contract F2).
  *   q_i8, k_i8  i8 [bh*seq, D]; sq, sk, sv f16 [bh*seq/32]; vt = the V^T operand image of
  *   qattn_int8_quant_vt; out O f16 [bh*seq, D]; lse f16 [bh*seq] (base 2).

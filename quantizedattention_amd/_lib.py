@@ -30,6 +30,7 @@ SIGNATURES = {
     "qattn_int8_quant_vt": [_vp, _vp, _vp, _vp, _c_long, _c_int, _vp],
     "qattn_int8_v_image": [_vp, _vp, _c_long, _c_int, _vp],
     "qattn_kmean": [_vp, _vp, _c_long, _c_long, _c_int, _vp],
+    "qattn_int8_quant_k_smooth": [_vp] * 5 + [_c_long, _c_long, _c_int, _vp],
     "qattn_int8_attn_fwd": [_vp] * 8 + [_c_long, _c_long, _c_int, _c_float, _vp],
     "qattn_int8_attn_fwd_ex": [_vp] * 8 + [_c_long, _c_long, _c_long, _c_int, _c_int, _c_int, _c_float,
                                                  _vp],

@@ -59,6 +59,11 @@ def _check_shapes(q, k, v):
         raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
 
 
+# k-smoothing through qattn_int8_quant_k_smooth (one launch) rather than qattn_kmean +
+# qattn_int8_quant_img (two); the outputs are bit-identical (tests/test_gpu_int8.py)
+FUSED_K_SMOOTH = True
+
+
 def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = False):
     """Quantise q, k, v and run the int8 attention forward (csrc/int8_attn_fwd.hip: both
     contractions on the int8 MFMA, P.V as the reference's hl.dot(P_int8, v_int8), int8:249).
@@ -92,15 +97,22 @@ def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = Fa
         q_bf = torch.empty((N, D), dtype=torch.bfloat16, device=dev)
         k_bf = torch.empty((Nkv, D), dtype=torch.bfloat16, device=dev)
     k_mean = None
-    if smooth:
-        k_mean = torch.empty((B, Hkv, 1, D), dtype=torch.float16, device=dev)
-        _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(k_mean), B * Hkv, Sk, D, st)
     qks = float(torch.tensor(_qk_scale(D), dtype=torch.float32))
     # k (smoothed, with the backward's bf16 image when asked), then v with its P.V operand image
     # (two launches: one launch alternating k and v workgroups measured 105 against 31 + 45 us at
-    # config 3)
-    _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
-              _lib.ptr(k_mean), Nkv, Sk, D, st)
+    # config 3, HISTORY.md round 5)
+    if smooth:
+        k_mean = torch.empty((B, Hkv, 1, D), dtype=torch.float16, device=dev)
+        if FUSED_K_SMOOTH:   # k-mean and the smoothed quantiser in one launch (bit-identical)
+            _lib.call("qattn_int8_quant_k_smooth", _lib.ptr(k), _lib.ptr(k_mean), _lib.ptr(k_i8),
+                      _lib.ptr(sk), _lib.ptr(k_bf), B * Hkv, Sk, D, st)
+        else:
+            _lib.call("qattn_kmean", _lib.ptr(k), _lib.ptr(k_mean), B * Hkv, Sk, D, st)
+            _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None,
+                      _lib.ptr(k_bf), _lib.ptr(k_mean), Nkv, Sk, D, st)
+    else:
+        _lib.call("qattn_int8_quant_img", _lib.ptr(k), _lib.ptr(k_i8), _lib.ptr(sk), None, _lib.ptr(k_bf),
+                  None, Nkv, Sk, D, st)
     _lib.call("qattn_int8_quant_vt", _lib.ptr(v), _lib.ptr(v_i8), _lib.ptr(sv), _lib.ptr(vt), Nkv, D, st)
     # q is quantised inside the attention kernel (q_i8, sq and the bf16 image written there)
     _lib.call("qattn_int8_attn_fwd_qf", _lib.ptr(q), _lib.ptr(q_i8), _lib.ptr(sq), _lib.ptr(q_bf),

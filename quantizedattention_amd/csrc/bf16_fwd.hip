@@ -38,13 +38,29 @@ namespace qattn {
 #ifndef QA_BF_FWD_WAVES
 #define QA_BF_FWD_WAVES 4   // waves (32 queries each) per workgroup
 #endif
+// (A/B) occupancy: waves per SIMD the register budget is sized for (2: <= 256 VGPRs, 3: <= 168),
+// ring slots (3 slots fit three 4-wave workgroups' rings in one CU's LDS), the two sub-tiles'
+// phases one after the other (SEQ: A0 B0 C0 A1 B1 C1) and QK^T of tile t+1 issued before the
+// softmax of tile t (PIPE)
+#ifndef QA_BF_FWD_OCC
+#define QA_BF_FWD_OCC 2
+#endif
+#ifndef QA_BF_FWD_NSLOT
+#define QA_BF_FWD_NSLOT 4
+#endif
+#ifndef QA_BF_FWD_SEQ
+#define QA_BF_FWD_SEQ 0
+#endif
+#ifndef QA_BF_FWD_PIPE
+#define QA_BF_FWD_PIPE 1
+#endif
 
 template <int D>
 struct Bf16FwdCfg {
   static constexpr int WAVES = QA_BF_FWD_WAVES;
   static constexpr int QROWS = 32 * WAVES;
   static constexpr int KT = 32;                 // keys per ring slot
-  static constexpr int NSLOT = 4;
+  static constexpr int NSLOT = QA_BF_FWD_NSLOT;
   static constexpr int ROWB = 2 * D;            // bytes per K / V row
   static constexpr int NCH = ROWB / 16;         // 16-B chunks per row
   static constexpr int TILE = KT * ROWB;        // bytes per K (or V) tile
@@ -55,7 +71,9 @@ struct Bf16FwdCfg {
   static constexpr int IPW = PIECES / WAVES;
   static constexpr int K_SHIFT = (D == 128) ? 0 : 1;   // K swizzle = (row >> K_SHIFT) & (NCH-1)
   static constexpr int V_SHIFT = (D == 128) ? 2 : 1;   // V swizzle = (row & 3) << V_SHIFT
-  static constexpr int STAGE_BYTES = WAVES * RowTile<D, float>::BYTES;
+  // output staging passes (two halves of the columns when the ring is 3 slots: 3 workgroups per CU)
+  static constexpr int STAGE_PASSES = NSLOT == 3 ? 2 : 1;
+  static constexpr int STAGE_BYTES = WAVES * RowTile<D, float, STAGE_PASSES>::BYTES;
   static constexpr int LDS = (NSLOT * SLOT > STAGE_BYTES) ? NSLOT * SLOT : STAGE_BYTES;
 };
 
@@ -157,7 +175,7 @@ __global__ __launch_bounds__(1024) void bf16_vsuffix_scan(float* __restrict__ ws
 }
 
 template <int D, bool CAUSAL, bool SFX>
-__global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
+__global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, QA_BF_FWD_OCC) void bf16_fwd_kernel(
     const _Float16* __restrict__ q, const _Float16* __restrict__ k, const __bf16* __restrict__ v,
     float* __restrict__ out, float* __restrict__ lse, int BH, int Sq, int Sk, int G, float qks,
     const float* __restrict__ vsuf) {
@@ -333,30 +351,57 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
   v16f acc = v16f{};
-  acc = qk(I0{});
-  // tile t lives in slot t & 3; at tile t the slot (t+1)&3 holds tile min(t+1, nt-1)
+  if (QA_BF_FWD_PIPE) acc = qk(I0{});
+  // tile t lives in slot t % NSLOT; at tile t the slot (t+1) % NSLOT holds tile min(t+1, nt-1)
   auto step = [&](auto SLc, auto NXc, auto FRc, int t) {
-    ring_wait_barrier<C::IPW>();   // tile t+1 landed (t+2 may be in flight); slot (t+3)&3 is free
-    dma.issue(smem_lds + decltype(FRc)::value * C::SLOT, min(t + 3, nte - 1));
+    // tile t+1 landed (later tiles may be in flight); slot (t + NSLOT - 1) % NSLOT is free
+    ring_wait_barrier<(C::NSLOT - 3) * C::IPW>();
+    dma.issue(smem_lds + decltype(FRc)::value * C::SLOT, min(t + C::NSLOT - 1, nte - 1));
     if (!(SFX && masked(t, 0))) {   // SFX: a tile past the wave's diagonal is in the suffix
       // (a tile masked for the whole wave needs no S: its QK^T MFMAs are skipped)
       v16f nacc = v16f{};
-      if (!masked(t + 1, 0)) nacc = qk(NXc);
-      Sub x0, x1;
-      phase_a(x0, t, 0, acc);
-      phase_a(x1, t, 1, acc);
-      phase_b(x0, masked(t, 0));
-      phase_b(x1, masked(t, 1));
-      phase_c(SLc, x0, 0);
-      phase_c(SLc, x1, 1);
-      acc = nacc;
+      if (QA_BF_FWD_PIPE) {
+        if (!masked(t + 1, 0)) nacc = qk(NXc);
+      } else if (!masked(t, 0)) {
+        acc = qk(SLc);
+      }
+      if (QA_BF_FWD_SEQ) {
+        {
+          Sub x0;
+          phase_a(x0, t, 0, acc);
+          phase_b(x0, masked(t, 0));
+          phase_c(SLc, x0, 0);
+        }
+        Sub x1;
+        phase_a(x1, t, 1, acc);
+        phase_b(x1, masked(t, 1));
+        phase_c(SLc, x1, 1);
+      } else {
+        Sub x0, x1;
+        phase_a(x0, t, 0, acc);
+        phase_a(x1, t, 1, acc);
+        phase_b(x0, masked(t, 0));
+        phase_b(x1, masked(t, 1));
+        phase_c(SLc, x0, 0);
+        phase_c(SLc, x1, 1);
+      }
+      if (QA_BF_FWD_PIPE) acc = nacc;
     }
   };
-  for (int t = 0; t < nte; t += 4) {
-    step(I0{}, I1{}, I3{}, t);
-    if (t + 1 < nte) step(I1{}, I2{}, I0{}, t + 1);
-    if (t + 2 < nte) step(I2{}, I3{}, I1{}, t + 2);
-    if (t + 3 < nte) step(I3{}, I0{}, I2{}, t + 3);
+  if constexpr (C::NSLOT == 4) {
+    for (int t = 0; t < nte; t += 4) {
+      step(I0{}, I1{}, I3{}, t);
+      if (t + 1 < nte) step(I1{}, I2{}, I0{}, t + 1);
+      if (t + 2 < nte) step(I2{}, I3{}, I1{}, t + 2);
+      if (t + 3 < nte) step(I3{}, I0{}, I2{}, t + 3);
+    }
+  } else {
+    static_assert(C::NSLOT == 3, "ring of 3 or 4 slots");
+    for (int t = 0; t < nte; t += 3) {
+      step(I0{}, I1{}, I2{}, t);
+      if (t + 1 < nte) step(I1{}, I2{}, I0{}, t + 1);
+      if (t + 2 < nte) step(I2{}, I0{}, I1{}, t + 2);
+    }
   }
   if constexpr (SFX) {
     // the masked keys K0 .. Sk-1 of this wave, all at once (see the header)
@@ -393,7 +438,8 @@ __global__ __launch_bounds__(64 * QA_BF_FWD_WAVES, 2) void bf16_fwd_kernel(
   const long row0 = (long)bh * Sq + q0;
   const float l = lacc[0];
   if (h == 0) lse[row0 + c32] = m + log2_f32(l);                 // bf16:288
-  store_rows<D, float>(o, 1.0f / l, smem + wave * RowTile<D, float>::BYTES, out + row0 * D, lane);
+  store_rows<D, float, C::STAGE_PASSES>(o, 1.0f / l, smem + wave * RowTile<D, float, C::STAGE_PASSES>::BYTES,
+                                        out + row0 * D, lane);
 }
 
 }  // namespace qattn

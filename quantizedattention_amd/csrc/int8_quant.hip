@@ -15,6 +15,11 @@
 
 namespace qattn {
 
+// workgroups per head of the fused k-mean + k quantiser (A/B)
+#ifndef QA_KQ_SPLITS
+#define QA_KQ_SPLITS 2
+#endif
+
 // max |x| over 8 fp16 values folded into a running pair of u16 maxima: for finite halves the order of
 // |x| is the integer order of (bits & 0x7fff), so one v_and + one v_pk_max_u16 per pair (the f32 form
 // takes a conversion and a max per value).  amax_pk_f32 turns the pair into the float max.
@@ -33,17 +38,15 @@ QA_DEVICE float amax_pk_f32(v2us acc) {
 // rows: total rows (multiple of 32); rows_per_head: S (for the k-mean lookup)
 // DEQ: also write f16(idx * s) (the forward's P.V operand for v); IMG: also write bf16(idx) (the
 // exact transposed-read image the backward's accumulating products use for q and k).
+// km: the block's head mean row (SMOOTH; global or LDS memory)
 template <int D, bool DEQ, bool SMOOTH, bool IMG>
 QA_DEVICE void quant_block32(const _Float16* __restrict__ x, int8_t* __restrict__ idx,
                              _Float16* __restrict__ scale, _Float16* __restrict__ deq,
-                             __bf16* __restrict__ img, const _Float16* __restrict__ kmean,
-                             long blk, int rows_per_head, int lane) {
+                             __bf16* __restrict__ img, const _Float16* km, long blk, int lane) {
   constexpr int ELEMS = 32 * D;        // elements per block
   constexpr int ITERS = ELEMS / 512;   // 8 halfs per lane per iteration
   const _Float16* xb = x + blk * ELEMS;
   v8h v[ITERS];
-  const _Float16* km = nullptr;
-  if constexpr (SMOOTH) km = kmean + (blk * 32 / rows_per_head) * D;
   v2us am = {0, 0};
 #pragma unroll
   for (int i = 0; i < ITERS; ++i) {
@@ -97,8 +100,8 @@ __global__ __launch_bounds__(256) void quant_block32_kernel(
     long nblocks, int rows_per_head) {
   const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blk >= nblocks) return;
-  quant_block32<D, DEQ, SMOOTH, IMG>(x, idx, scale, deq, img, kmean, blk, rows_per_head,
-                                     threadIdx.x & 63);
+  const _Float16* km = SMOOTH ? kmean + (blk * 32 / rows_per_head) * D : nullptr;
+  quant_block32<D, DEQ, SMOOTH, IMG>(x, idx, scale, deq, img, km, blk, threadIdx.x & 63);
 }
 
 // ------------------------------------------------------------ V with the int8 P.V operand image
@@ -208,9 +211,81 @@ __global__ __launch_bounds__(1024) void kmean_kernel(const _Float16* __restrict_
   }
 }
 
+// k-mean and the smoothed k quantiser in one launch (the two passes of qattn_kmean +
+// qattn_int8_quant_img with kmean): SPLITS 1024-thread workgroups per head each sum the whole head
+// (kmean_kernel's arithmetic and order, so k_mean is bit-identical; the repeated reads of a head
+// hit the L2 / Infinity Cache), keep the mean in LDS, and quantise their 1/SPLITS of the head's
+// 32-row blocks from the cache with it.  Split 0 writes k_mean.
+template <int D, bool IMG, int SPLITS>
+__global__ __launch_bounds__(1024) void kmean_quant_kernel(const _Float16* __restrict__ k,
+                                                           _Float16* __restrict__ kmean,
+                                                           int8_t* __restrict__ idx,
+                                                           _Float16* __restrict__ scale,
+                                                           __bf16* __restrict__ img, int S) {
+  constexpr int TPR = D / 8;
+  constexpr int RPI = 1024 / TPR;
+  constexpr int U = 4;
+  __shared__ float part[RPI][D + 1];
+  __shared__ __attribute__((aligned(16))) _Float16 km[D];
+  const int bh = blockIdx.x / SPLITS, sp = blockIdx.x % SPLITS;
+  const int t = threadIdx.x;
+  const int c = (t % TPR) * 8, r0 = t / TPR;
+  const _Float16* kb = k + (long)bh * S * D;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int r = r0;
+  for (; r + (U - 1) * RPI < S; r += U * RPI) {
+    v8h x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = *reinterpret_cast<const v8h*>(kb + (long)(r + u * RPI) * D + c);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)x[u][j];
+  }
+  for (; r < S; r += RPI) {
+    const v8h x = *reinterpret_cast<const v8h*>(kb + (long)r * D + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += (float)x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[r0][c + j] = acc[j];
+  __syncthreads();
+  if (t < D) {
+    float sum = 0.f;
+    for (int i = 0; i < RPI; ++i) sum += part[i][t];
+    const _Float16 m = (_Float16)(sum / (float)S);
+    km[t] = m;
+    if (sp == 0) kmean[(long)bh * D + t] = m;
+  }
+  __syncthreads();
+  const int nb = S / 32, per = (nb + SPLITS - 1) / SPLITS;
+  const int b1 = min(nb, (sp + 1) * per);
+  for (int b = sp * per + (t >> 6); b < b1; b += 16)
+    quant_block32<D, false, true, IMG>(k, idx, scale, nullptr, img, km, (long)bh * nb + b, t & 63);
+}
+
 }  // namespace qattn
 
 using namespace qattn;
+
+extern "C" int qattn_int8_quant_k_smooth(const void* k, void* kmean, void* k_i8, void* sk, void* k_bf,
+                                         long bh, long seq, int head_dim, void* stream) {
+  if (seq % 32 != 0 || (head_dim != 64 && head_dim != 128)) return 1;
+  if (bh == 0 || seq == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  constexpr int SP = QA_KQ_SPLITS;
+  const dim3 grid((unsigned)(bh * SP)), block(1024);
+#define QA_LAUNCH(Dv, IM)                                                                              \
+  hipLaunchKernelGGL((kmean_quant_kernel<Dv, IM, SP>), grid, block, 0, st, (const _Float16*)k,        \
+                     (_Float16*)kmean, (int8_t*)k_i8, (_Float16*)sk, (__bf16*)k_bf, (int)seq)
+  if (head_dim == 128) {
+    if (k_bf) QA_LAUNCH(128, true); else QA_LAUNCH(128, false);
+  } else {
+    if (k_bf) QA_LAUNCH(64, true); else QA_LAUNCH(64, false);
+  }
+#undef QA_LAUNCH
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 extern "C" int qattn_int8_quant_img(const void* x, void* idx, void* scale, void* deq, void* img,
                                     const void* kmean, long rows, int rows_per_head, int head_dim,

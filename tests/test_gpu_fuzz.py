@@ -6,13 +6,13 @@ net.
 
 Bars: quantisation bit-exact; O within the north star's 1e-2 of the oracle (scaled by
 |v| / 4 where |v| > 4) and no further from exact fp32 attention than the oracle is (+1e-2, scaled);
-lse within 2 fp16 steps; grads relL2 <= 0.05 vs the oracle; the cached (decoding) forward within
+lse within 2 fp16 steps; grads relL2 <= conftest.INT8_BWD_REL_FUZZ (0.045) vs the oracle; the cached (decoding) forward within
 2e-3 |v| of the forward."""
 
 import pytest
 import torch
 
-from conftest import INT8_BWD_REL
+from conftest import INT8_BWD_REL_FUZZ
 
 from oracle import restate as R
 
@@ -83,7 +83,7 @@ def test_int8_fuzz(lib, i):
         assert torch.isfinite(a).all(), name
         rel = ((a - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
         print(f"RELL2 int8-bwd-vs-oracle {name} {rel:.5f}")
-        assert rel <= INT8_BWD_REL, (name, rel)
+        assert rel <= INT8_BWD_REL_FUZZ, (name, rel)
     # the decoding layout on the same operands (non-causal, head_dim 128)
     if not causal and D == 128:
         from quantizedattention_amd.kv_cache import attention_int8_cached, quantize_kv

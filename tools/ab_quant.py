@@ -50,11 +50,24 @@ fns = {
     "quant_img(k, smooth)": lambda: call("qattn_int8_quant_img", P(k), P(ki), P(sk), None, P(kb), P(km),
                                          N, S, D, st),
     "quant_vt(v)": lambda: call("qattn_int8_quant_vt", P(v), P(vi), P(sv), P(vt), N, D, st),
+    "quant(k, smooth, no img)": lambda: call("qattn_int8_quant_img", P(k), P(ki), P(sk), None, None, P(km),
+                                             N, S, D, st),
+    "kmean+quant(k) 2 launches": lambda: (call("qattn_kmean", P(k), P(km), B * H, S, D, st),
+                                          call("qattn_int8_quant_img", P(k), P(ki), P(sk), None, None, P(km),
+                                               N, S, D, st)),
+    "k_smooth fused": lambda: call("qattn_int8_quant_k_smooth", P(k), P(km), P(ki), P(sk), None, B * H, S, D,
+                                   st),
+    "k_smooth fused +img": lambda: call("qattn_int8_quant_k_smooth", P(k), P(km), P(ki), P(sk), P(kb), B * H,
+                                        S, D, st),
     "bwd_prep": lambda: call("qattn_int8_bwd_prep", P(dO), P(O), P(lse), P(di), P(sd), P(LD), P(db),
                              B * H, S, D, st),
 }
 bytes_of = {"kmean": N * D * 2, "quant_img(q)": N * D * 5, "quant_img(k, smooth)": N * D * 5,
-            "quant_vt(v)": N * D * 4, "bwd_prep": N * D * 7 + N * 10}
+            "quant_vt(v)": N * D * 4, "bwd_prep": N * D * 7 + N * 10, "quant(k, smooth, no img)": N * D * 3,
+            "kmean+quant(k) 2 launches": N * D * 5, "k_smooth fused": N * D * 3, "k_smooth fused +img": N * D * 5}
+if getattr(lib, "qattn_int8_quant_k_smooth", None) is None:   # (an older library)
+    for n_ in ("k_smooth fused", "k_smooth fused +img"):
+        fns.pop(n_)
 res = {}
 for name, f in fns.items():
     for _ in range(3):
