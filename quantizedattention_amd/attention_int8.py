@@ -59,9 +59,10 @@ def _check_shapes(q, k, v):
         raise _lib.QAttnError("qattn int8: head_dim must be 64 or 128")
 
 
-# k-smoothing through qattn_int8_quant_k_smooth (one launch) rather than qattn_kmean +
-# qattn_int8_quant_img (two); the outputs are bit-identical (tests/test_gpu_int8.py)
-FUSED_K_SMOOTH = True
+# k-smoothing through qattn_int8_quant_k_smooth (one launch) instead of qattn_kmean +
+# qattn_int8_quant_img (two): bit-identical (tests/test_gpu_int8.py), and no faster at config 3 (55
+# against 54.5 us, 88 against ~83 us with the backward's image; HISTORY.md round 6), so off
+FUSED_K_SMOOTH = False
 
 
 def _int8_forward(q, k, v, smooth: bool, images: bool = False, causal: bool = False):

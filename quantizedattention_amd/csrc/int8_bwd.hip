@@ -216,6 +216,12 @@ enum BwdRole { ROLE_DV = 0, ROLE_DK = 1, ROLE_DQ = 2, ROLE_DKV = 3 };
 #ifndef QA_DQW_HG   // (the same for the causal dQ-from-records grid)
 #define QA_DQW_HG 0
 #endif
+#ifndef QA_DKV_PRIO
+#define QA_DKV_PRIO 0
+#endif
+#ifndef QA_DQW_PRIO
+#define QA_DQW_PRIO 0
+#endif
 #ifndef QA_BWD_PACK_ASM
 #define QA_BWD_PACK_ASM 1
 #endif
@@ -720,6 +726,10 @@ void int8_bwd_kernel(
     // instructions per tile-wave).  Grouped heads stream the group's query heads one after another,
     // so their diagonals recur: masked throughout.
     const int tb = !CAUSAL ? t0 : (Ny == Smod ? min(nt, t0 + G::WAVES) : nt);
+    // (A/B) static priority for one half of the workgroup (MI355X_MICROARCH "Two waves per SIMD",
+    // item 4): QA_DKV_PRIO = 1 raises waves 4-7 (the staggered half), 2 waves 0-3
+    if (QA_DKV_PRIO == 1 && wave >= G::WAVES / 2) __builtin_amdgcn_s_setprio(1);
+    if (QA_DKV_PRIO == 2 && wave < G::WAVES / 2) __builtin_amdgcn_s_setprio(1);
     if (QA_DKV_PIPE || (QA_DKV_STAGGER && wave >= G::WAVES / 2)) {
       // DKV pipelined: carry the quantised bf16 operands of tile t (16 VGPRs) into iteration t, whose
       // int8 products for tile t+1 are issued first and whose fp32 values of t+1 are computed beside
@@ -1023,6 +1033,7 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
   // on its own VALU chain.  Same operations as the unpipelined order: dq is bit-identical.
   v8bf op[2];
   if (active) make_op(0, op);
+  if (QA_DQW_PRIO && wave >= W::WAVES / 2) __builtin_amdgcn_s_setprio(1);   // (A/B, as QA_DKV_PRIO)
   for (int t = 0; t < nt; ++t) {
     // tile t's k image and tile t+1's record landed: with RSLOT - 1 = NSLOT both were issued three
     // iterations ago, and younger than them are the k + record DMAs of the two iterations since

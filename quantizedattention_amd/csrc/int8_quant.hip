@@ -15,9 +15,10 @@
 
 namespace qattn {
 
-// workgroups per head of the fused k-mean + k quantiser (A/B)
+// workgroups per head of the fused k-mean + k quantiser (A/B: 1 55.1-55.4 us, 2 71-72, 4 107-109 at
+// config 3 against 54.5 us for qattn_kmean + qattn_int8_quant_img; HISTORY.md round 6)
 #ifndef QA_KQ_SPLITS
-#define QA_KQ_SPLITS 2
+#define QA_KQ_SPLITS 1
 #endif
 
 // max |x| over 8 fp16 values folded into a running pair of u16 maxima: for finite halves the order of

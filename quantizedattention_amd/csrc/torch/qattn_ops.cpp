@@ -163,17 +163,14 @@ T8 int8_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, bool smo
     lse.zero_();
     return {O, lse, q_i8, k_i8, v_i8, sq, sk, sv};
   }
-  if (smooth) {   // k-mean and the smoothed k quantiser in one launch
+  if (smooth) {
     k_mean = empty({B, Hkv, 1, D}, at::kHalf, q);
-    call(qattn_int8_quant_k_smooth(P(k), P(k_mean), P(k_i8), P(sk), nullptr, B * Hkv, Sk, (int)D,
-                                   c.stream),
-         "kmean + quantise k");
-  } else {
-    call(qattn_int8_quant(P(k), P(k_i8), P(sk), nullptr, nullptr, Nkv, (int)Sk, (int)D, c.stream),
-         "quantise k");
+    call(qattn_kmean(P(k), P(k_mean), B * Hkv, Sk, (int)D, c.stream), "kmean");
   }
 
   const float qks = qk_scale(D);
+  call(qattn_int8_quant(P(k), P(k_i8), P(sk), nullptr, P(k_mean), Nkv, (int)Sk, (int)D, c.stream),
+       "quantise k");
   call(qattn_int8_quant_vt(P(v), P(v_i8), P(sv), P(vt), Nkv, (int)D, c.stream), "quantise v");
   call(qattn_int8_attn_fwd_qf(P(q), P(q_i8), P(sq), nullptr, P(k_i8), P(sk), P(vt), P(sv), P(O), P(lse),
                               B * H, S, Sk, (int)(H / Hkv), causal ? 1 : 0, (int)D, qks, c.stream),

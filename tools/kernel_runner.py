@@ -74,6 +74,10 @@ for name in [n for _ in range(reps) for n in names]:
     elif name == "int8_dkdv_ws":
         _lib.call("qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv),
                   P(LD), P(qb), P(ob), P(dk), P(dv), P(ws), B * H, S, D, qks, sms, st)
+    elif name == "int8_dkdv_ws_2048":   # non-causal workgroups of 64 query tiles (the causal average at
+        # S = 4096 is 68): the per-tile counters beside int8_bwd_causal's (operands re-used as S = 2048)
+        _lib.call("qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv),
+                  P(LD), P(qb), P(ob), P(dk), P(dv), P(ws), B * H, 2048, D, qks, sms, st)
     elif name == "int8_dkdv_wsc":   # one launch of the step's chunked record backward (CHUNK heads)
         _lib.call("qattn_int8_bwd_dkdv_ws", P(dOi), P(sdO), P(qi), P(sq), P(ki), P(sk), P(vi), P(sv),
                   P(LD), P(qb), P(ob), P(dk), P(dv), P(ws), CHUNK, S, D, qks, sms, st)
