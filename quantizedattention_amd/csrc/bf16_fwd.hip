@@ -14,12 +14,11 @@
 // mask each); "#{S >= thr} > 1" is evaluated as "second-largest S of the row >= thr", with the
 // row's top two values carried by v_max / v_med3 (the largest is the row max the rule needs anyway).
 //
-// Structure (as int8_attn_fwd.hip): 4 waves x 32 query rows per workgroup; 32-key K/V tiles
-// stream through a 4-slot LDS ring filled by buffer LDS-DMA (one barrier per tile); swapped QK^T
-// (keys in registers, one query per lane pair) so P feeds the PV MFMA straight from registers;
-// V read column-wise with ds_read_b64_tr_b16.  One 16-key sub-tile == one k-step of the
-// 32x32x16 PV MFMA.  Software pipeline: the QK^T MFMAs of tile t+1 are issued before the
-// softmax of tile t.
+// Structure (as int8_attn_fwd.hip): 4 waves x 32 query rows per workgroup, three workgroups per CU
+// (three waves per SIMD); 32-key K/V tiles stream through a 3-slot LDS ring filled by buffer
+// LDS-DMA (one barrier per tile); swapped QK^T (keys in registers, one query per lane pair) so P
+// feeds the PV MFMA straight from registers; V read column-wise with ds_read_b64_tr_b16.  One
+// 16-key sub-tile == one k-step of the 32x32x16 PV MFMA.
 //
 // Causal with a V-suffix workspace (qattn_bf16_fwd_ws_ex): past a wave's diagonal tile every score
 // is the fill value -126, the running max can no longer move (the diagonal tile already holds the
@@ -38,21 +37,23 @@ namespace qattn {
 #ifndef QA_BF_FWD_WAVES
 #define QA_BF_FWD_WAVES 4   // waves (32 queries each) per workgroup
 #endif
-// (A/B) occupancy: waves per SIMD the register budget is sized for (2: <= 256 VGPRs, 3: <= 168),
-// ring slots (3 slots fit three 4-wave workgroups' rings in one CU's LDS), the two sub-tiles'
-// phases one after the other (SEQ: A0 B0 C0 A1 B1 C1) and QK^T of tile t+1 issued before the
-// softmax of tile t (PIPE)
+// Occupancy (round 6): three waves per SIMD (<= 168 VGPRs; OCC), a 3-slot ring (three 4-wave
+// workgroups' rings and output staging fit one CU's LDS; NSLOT), the two sub-tiles' phases one after
+// the other (SEQ: A0 B0 C0 A1 B1 C1) and no QK^T one tile ahead (PIPE = 0): the third wave covers the
+// latency the software pipeline and the interleaved sub-tiles covered before, in 164 instead of 188
+// VGPRs at D = 128 (no spills).  Bit-identical; 2-6 % faster at configs 2 and 3, causal included
+// (profiles/r06_bf16_fwd_3wave_ab.log).  The round-5 form is OCC 2, NSLOT 4, SEQ 0, PIPE 1.
 #ifndef QA_BF_FWD_OCC
-#define QA_BF_FWD_OCC 2
+#define QA_BF_FWD_OCC 3
 #endif
 #ifndef QA_BF_FWD_NSLOT
-#define QA_BF_FWD_NSLOT 4
+#define QA_BF_FWD_NSLOT 3
 #endif
 #ifndef QA_BF_FWD_SEQ
-#define QA_BF_FWD_SEQ 0
+#define QA_BF_FWD_SEQ 1
 #endif
 #ifndef QA_BF_FWD_PIPE
-#define QA_BF_FWD_PIPE 1
+#define QA_BF_FWD_PIPE 0
 #endif
 
 template <int D>
