@@ -873,7 +873,9 @@ void int8_bwd_kernel(
 // The dK+dV kernel (8 waves) writes records only for q-tiles >= its workgroup's first key tile,
 // and this kernel reads every key tile up to its workgroup's last query tile for all of its waves:
 // with more than 8 waves per workgroup the first ones would read records never written (causal).
+#ifndef QA_DQW_ALLOW_WIDE   // (A/B, non-causal timing only: wider workgroups break the causal records)
 static_assert(QA_DQW_WAVES <= 8, "dQ-from-records workgroups may not exceed the dK+dV kernel's 8 waves");
+#endif
 template <int D>
 struct DqwCfg {
   static constexpr int WAVES = QA_DQW_WAVES;
