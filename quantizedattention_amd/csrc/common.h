@@ -39,8 +39,12 @@ typedef int v2i __attribute__((ext_vector_type(2)));
 // kernel instantiation), so steady-state launches (decode steps of ~50 us) make no attribute call.
 inline bool lds_grant(const void* kernel, int bytes, int& granted) {
   if (bytes <= granted) return true;
-  if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+  if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
+    // clear the runtime's last error: the caller reports the refusal (status 1), and a stale
+    // hipErrorInvalidValue would otherwise surface in the host program's next unrelated HIP call
+    (void)hipGetLastError();
     return false;
+  }
   granted = bytes;
   return true;
 }

@@ -105,6 +105,10 @@ struct SmTile {
 #ifndef QA_FWD_ABL
 #define QA_FWD_ABL 0
 #endif
+// tiles between two foldings of the KMAG bias out of O (rebias in the body; 0 = never)
+#ifndef QA_FWD_REBIAS
+#define QA_FWD_REBIAS 32
+#endif
 #ifndef QA_FWD_DQ_SCALAR
 #define QA_FWD_DQ_SCALAR 0
 #endif
@@ -275,7 +279,8 @@ QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
   // per-tile scales, shifted by one tile: entry i holds tile min(i + 1, nt - 1), the tile whose SM1
   // runs in loop iteration i, so that 4 iterations read their scales with one 16-B LDS read
   float* svq_lds = ck_lds + ((nt + 3) & ~3);
-  // the exp2 correction table of the literal chain (exp2_corr.h), after the scale tables
+  // the exp2 correction table of the literal chain (exp2_corr.h), after the scale tables; in the
+  // fast pass (DEFER) the same region holds the deferred votes instead (the table is not loaded)
   unsigned* corr_lds = reinterpret_cast<unsigned*>(svq_lds + ((nt + 3) & ~3));
 
   DmaPlan<D> dma;
@@ -422,6 +427,23 @@ QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
       }
     obias += cpv;
   };
+  // Fold the KMAG bias out of O every QA_FWD_REBIAS tiles: O holds sum_t (KMAG + X_t) c_t, whose
+  // magnitude grows with the tiles while the signal sum_t X_t c_t does not, so without it the fp32
+  // rounding of the accumulator (correlated from tile to tile: the same c_t) eats the signal on long
+  // key ranges (relL2 0.16 against exact attention at 128k keys).  O - KMAG * obias in one fma per
+  // element (the product exact inside it); then obias restarts from 0.
+  auto rebias = [&]() {
+    const v2f_ nk = {-KMAG, -KMAG}, ob = {obias, obias};
+#pragma unroll
+    for (int b = 0; b < C::NDB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const v2f_ y = __builtin_elementwise_fma(nk, ob, v2f_{o[b][r], o[b][r + 1]});
+        o[b][r] = y[0];
+        o[b][r + 1] = y[1];
+      }
+    obias = 0.f;
+  };
 
   // first half of the softmax of tile t: row max, d = f16(S - rm), deferred running max, er, the
   // tile's P.V scale, and the literal-chain vote
@@ -517,7 +539,7 @@ QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
     if (DEFER && lit) {   // write the vote down (a wave-uniform branch); the tile stays fast
       if (nvote < C::NV) {
         const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        unsigned* cs = corr_lds + EXP2_CORR_WORDS + (wave * C::NV + nvote) * 128 + ln;
+        unsigned* cs = corr_lds + (wave * C::NV + nvote) * 128 + ln;   // (over the unloaded table)
         cs[0] = __float_as_uint(st.er);
         cs[64] = (unsigned)__builtin_bit_cast(unsigned short, m);
       }
@@ -628,13 +650,18 @@ QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
       iter(t + 1, 1, 2, 0, ck4[1], sv4[1], nodiag, 1);
       iter(t + 2, 2, 3, 1, ck4[2], sv4[2], nodiag, 2);
       iter(t + 3, 3, 0, 2, ck4[3], sv4[3], nodiag, 3);
+      if (QA_FWD_REBIAS > 0 && ((t + 4) % QA_FWD_REBIAS) == 0) rebias();
     }
-    for (; t < tmain; ++t)
+    for (; t < tmain; ++t) {
       iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], nodiag, -2);
+      if (QA_FWD_REBIAS > 0 && ((t + 1) % QA_FWD_REBIAS) == 0) rebias();
+    }
     if constexpr (CAUSAL) {
-      for (; t < nt; ++t)
+      for (; t < nt; ++t) {
         iter(t, t & 3, (t + 1) & 3, (t + 3) & 3, ck_lds[t], svq_lds[t], std::true_type{},
              -2);
+        if (QA_FWD_REBIAS > 0 && ((t + 1) % QA_FWD_REBIAS) == 0) rebias();
+      }
     }
   } else {   // a wave past the last query row: the barriers and the ring's DMA only
     for (int t = 0; t < nt; ++t) {
@@ -655,7 +682,7 @@ QA_DEVICE __attribute__((always_inline)) void int8_attn_fwd_body(
       fix = true;
     } else {
       const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-      const unsigned* cs = corr_lds + EXP2_CORR_WORDS + wave * C::NV * 128 + ln;
+      const unsigned* cs = corr_lds + wave * C::NV * 128 + ln;
       bool any = false;
 #pragma unroll
       for (int c = 0; c < C::NV; ++c) {

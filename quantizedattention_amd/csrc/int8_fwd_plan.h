@@ -58,8 +58,11 @@ struct Int8FwdCfg {
   static constexpr int NV = QA_FWD_DEFER > 0 ? QA_FWD_DEFER : 1;   // deferred-vote slots per wave
   static constexpr int CAND_BYTES = WAVES * NV * 128 * 4;           // {er, m} per lane and slot
   // LDS bytes of a launch over nt key tiles: ring, two per-tile scale tables (padded to 4 tiles),
-  // the correction table, the deferred vote
-  static constexpr int lds_bytes(int nt) { return RING + ((nt + 3) / 4 * 4) * 8 + CORR_BYTES + CAND_BYTES; }
+  // then one region that holds the deferred votes in the fast pass and the correction table in the
+  // fixup pass (the fast pass never loads the table; the inline fixup loads it after the fast pass's
+  // epilogue has read its votes and the workgroup has passed a barrier)
+  static constexpr int VOTE_OR_CORR = CORR_BYTES > CAND_BYTES ? CORR_BYTES : CAND_BYTES;
+  static constexpr int lds_bytes(int nt) { return RING + ((nt + 3) / 4 * 4) * 8 + VOTE_OR_CORR; }
 };
 
 template <int D>
