@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "qattn.h"  // the C ABI: every extern "C" definition is checked against its declaration
 
 namespace qattn {
@@ -50,6 +52,17 @@ inline bool lds_grant(const void* kernel, int bytes, int& granted) {
 }
 
 // ---------------------------------------------------------------- MFMA wrappers
+// f(std::integral_constant<int, 0>{}) .. f(std::integral_constant<int, N - 1>{}): a loop body
+// instantiated per index, so ring slots and similar indices are compile-time constants in it
+template <typename F, int... I>
+QA_DEVICE void static_for_seq(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+QA_DEVICE void static_for(F&& f) {
+  static_for_seq(f, std::make_integer_sequence<int, N>{});
+}
+
 QA_DEVICE v16i mfma_i8(v4i a, v4i b, v16i c) {
   return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
 }

@@ -857,6 +857,11 @@ void int8_bwd_kernel(
 #ifndef QA_DQW_WAVES
 #define QA_DQW_WAVES 8
 #endif
+// Timing-only diagnostics (results wrong): every tile's record load reads the wave's first record
+// (bit 1: no HBM record stream), every k-image load reads the head's first key tile (bit 2)
+#ifndef QA_DQW_DIAG
+#define QA_DQW_DIAG 0
+#endif
 #ifndef QA_DQW_NT
 #define QA_DQW_NT 1
 #endif
@@ -939,25 +944,26 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
   auto issue_k = [&](int t) {
     const unsigned sl = smem_lds + (t % W::NSLOT) * W::T16;
 #pragma unroll
-    for (int i = 0; i < W::IPK; ++i) dma16_buf(krsrc[i], kvoff[i], (unsigned)min(t, nt - 1) * 64u * D, sl + klds[i]);
+    for (int i = 0; i < W::IPK; ++i)
+      dma16_buf(krsrc[i], kvoff[i], (QA_DQW_DIAG & 2) ? 0u : (unsigned)min(t, nt - 1) * 64u * D, sl + klds[i]);
   };
-  auto issue_r = [&](int t) {   // each record is read once: non-temporal
+  auto issue_r = [&](int t, int rs) {   // record of tile t into ring slot rs; read once: non-temporal
 #if QA_DQW_NT
-    dma16_buf_nt(rrsrc, 16u * lane, (unsigned)min(t, nt - 1) * 1024u,
+    dma16_buf_nt(rrsrc, 16u * lane, (QA_DQW_DIAG & 1) ? 0u : (unsigned)min(t, nt - 1) * 1024u,
 #else
-    dma16_buf(rrsrc, 16u * lane, (unsigned)min(t, nt - 1) * 1024u,
+    dma16_buf(rrsrc, 16u * lane, (QA_DQW_DIAG & 1) ? 0u : (unsigned)min(t, nt - 1) * 1024u,
 #endif
-              smem_lds + W::RBASE + (t % W::RSLOT) * W::REC + wave * 1024);
+              smem_lds + W::RBASE + rs * W::REC + wave * 1024);
   };
 #pragma unroll
   for (int i = 0; i < W::NSLOT - 1; ++i) issue_k(i);
-  for (int i = 0; i < W::RSLOT - 1; ++i) issue_r(i);
-  // per-tile scales: s_dS of each wave's records, sk of the key tiles (once, in LDS)
-  float* sds_lds = reinterpret_cast<float*>(smem + W::RBASE + W::RSLOT * W::REC);
-  _Float16* sk_lds = reinterpret_cast<_Float16*>(sds_lds + W::WAVES * nkt);
-  if (active)
-    for (int i = lane; i < nt; i += 64) sds_lds[wave * nkt + i] = sds[rec0 + i];
-  for (int i = tid; i < nt; i += 64 * W::WAVES) sk_lds[i] = sk[kv_row0 / 32 + i];
+#pragma unroll
+  for (int i = 0; i < W::RSLOT - 1; ++i) issue_r(i, i);
+  // per-tile operand scales s_dS * sk of each wave's records, once, in LDS (0 for an inactive
+  // wave, whose zero records then give zero operands; one padding float after the last wave's for
+  // the discarded operand of the loop's last iteration)
+  float* c_lds = reinterpret_cast<float*>(smem + W::RBASE + W::RSLOT * W::REC);
+  for (int i = lane; i < nt; i += 64) c_lds[wave * nkt + i] = active ? sds[rec0 + i] * (float)sk[kv_row0 / 32 + i] : 0.f;
 
 #if QA_DQW_TR8
   // ds_read_b64_tr_b8 of the record (per 16-lane group: lane 2j+p reads bytes 8p..8p+7 of row j,
@@ -995,12 +1001,12 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
 #pragma unroll
   for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
 
-  // the bf16 operand of tile t: its record brought into dQ order by the permutation MFMA (exact
-  // integers), scaled by s_dS * sk
-  auto make_op = [&](int t, v8bf* op) {
-    const float c = sds_lds[wave * nkt + t] * (float)sk_lds[t];
+  // the bf16 operand of tile t (its record in ring slot rs): the record brought into dQ order by
+  // the permutation MFMA (exact integers), scaled by s_dS * sk
+  auto make_op = [&](int t, int rs, v8bf* op) {
+    const float c = c_lds[wave * nkt + t];
 #if QA_DQW_TR8
-    const char* rb = smem + W::RBASE + (t % W::RSLOT) * W::REC + wave * 1024 + rtr;
+    const char* rb = smem + W::RBASE + rs * W::REC + wave * 1024 + rtr;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const v2i x = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
@@ -1014,8 +1020,8 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
       op[s] = __builtin_bit_cast(v8bf, w);
     }
 #else
-    const v4i rec = *reinterpret_cast<const v4i*>(smem + W::RBASE + (t % W::RSLOT) * W::REC +
-                                                  wave * 1024 + 16 * (lane ^ ((lane >> 5) << 2)));
+    const v4i rec = *reinterpret_cast<const v4i*>(smem + W::RBASE + rs * W::REC + wave * 1024 +
+                                                  16 * (lane ^ ((lane >> 5) << 2)));
     const v16i x = mfma_i8(rec, perm, v16i{});   // dS_i8 in dQ order (exact integers)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1033,37 +1039,49 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
   // Software-pipelined by one tile: the operand of tile t+1 (record read, permutation MFMA, 16
   // conversions) is formed beside the 8 bf16 MFMAs of tile t, so a wave's MFMA chain does not wait
   // on its own VALU chain.  Same operations as the unpipelined order: dq is bit-identical.
+  // Every wave runs the loop (an inactive one on zero records and scales, stored nowhere), and the
+  // loop is unrolled by the record ring's RSLOT with its slots as constants, so the tile step has no
+  // branch and no modulo of the ring index.
   v8bf op[2];
-  if (active) make_op(0, op);
+  make_op(0, 0, op);
   if (QA_DQW_PRIO && wave >= W::WAVES / 2) __builtin_amdgcn_s_setprio(1);   // (A/B, as QA_DKV_PRIO)
-  for (int t = 0; t < nt; ++t) {
+  // tile t; rs_next = (t + 1) % RSLOT, rs_issue = (t + RSLOT - 1) % RSLOT
+  auto step = [&](int t, int rs_next, int rs_issue) {
     // tile t's k image and tile t+1's record landed: with RSLOT - 1 = NSLOT both were issued three
     // iterations ago, and younger than them are the k + record DMAs of the two iterations since
     // (records more than one tile ahead of the k image: tile t's k image binds, and its
     // iteration's record DMA is younger)
     ring_wait_barrier<(W::RSLOT - 1 > W::NSLOT ? 1 : 0) + (W::NSLOT - 2) * (W::IPK + 1)>();
     issue_k(t + W::NSLOT - 1);
-    issue_r(t + W::RSLOT - 1);
-    if (active) {
-      const char* kb = smem + (t % W::NSLOT) * W::T16;
-      v8bf ta[2 * C::NDB];
+    issue_r(t + W::RSLOT - 1, rs_issue);
+    const char* kb = smem + (t % W::NSLOT) * W::T16;
+    v8bf ta[2 * C::NDB];
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int b = 0; b < C::NDB; ++b) {
-          const char* a = kb + troff[b] + 16 * s * 2 * D;
-          ta[s * C::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * 2 * D));
-        }
-      v8bf opn[2];
-      make_op(min(t + 1, nt - 1), opn);   // (the last iteration re-forms tile nt-1's: discarded)
+      for (int b = 0; b < C::NDB; ++b) {
+        const char* a = kb + troff[b] + 16 * s * 2 * D;
+        ta[s * C::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * 2 * D));
+      }
+    // (the last iteration forms an operand from slot nt % RSLOT and the scale after the wave's
+    // last: discarded)
+    v8bf opn[2];
+    make_op(t + 1, rs_next, opn);
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int b = 0; b < C::NDB; ++b) acc[b] = mfma_bf16(ta[s * C::NDB + b], op[s], acc[b]);
-      op[0] = opn[0];
-      op[1] = opn[1];
-    }
+      for (int b = 0; b < C::NDB; ++b) acc[b] = mfma_bf16(ta[s * C::NDB + b], op[s], acc[b]);
+    op[0] = opn[0];
+    op[1] = opn[1];
+  };
+  int t = 0;
+  for (; t + W::RSLOT <= nt; t += W::RSLOT) {
+    static_for<W::RSLOT>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      step(t + j, (j + 1) % W::RSLOT, (j + W::RSLOT - 1) % W::RSLOT);
+    });
   }
+  for (; t < nt; ++t) step(t, (t + 1) % W::RSLOT, (t + W::RSLOT - 1) % W::RSLOT);
   vmcnt_wait_all();
   if (!active) return;
 #if QA_DQW_TR8
@@ -1156,7 +1174,7 @@ static void launch_dqw_c(const void* ds8, const void* sds, const void* k_bf, con
                          long bh, long sqt, long skt, int group, float sms, hipStream_t st) {
   using G = DqwCfg<D>;
   const int nkt = (int)(skt / 32);
-  const int lds = G::RBASE + G::RSLOT * G::REC + G::WAVES * nkt * 4 + (nkt * 2 + 15) / 16 * 16;
+  const int lds = G::RBASE + G::RSLOT * G::REC + G::WAVES * nkt * 4 + 16;
   { static int granted_ = 0; lds_grant((const void*)int8_bwd_dqw_kernel<D, CAUSAL>, lds, granted_); }
   const int nb = (int)((sqt + 32 * G::WAVES - 1) / (32 * G::WAVES));
   hipLaunchKernelGGL((int8_bwd_dqw_kernel<D, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
