@@ -858,7 +858,8 @@ void int8_bwd_kernel(
 #define QA_DQW_WAVES 8
 #endif
 // Timing-only diagnostics (results wrong): every tile's record load reads the wave's first record
-// (bit 1: no HBM record stream), every k-image load reads the head's first key tile (bit 2)
+// (bit 1: no HBM record stream), every k-image load reads the head's first key tile (bit 2); no
+// record DMA at all (bit 4), no k-image DMA at all (bit 8)
 #ifndef QA_DQW_DIAG
 #define QA_DQW_DIAG 0
 #endif
@@ -945,9 +946,10 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
     const unsigned sl = smem_lds + (t % W::NSLOT) * W::T16;
 #pragma unroll
     for (int i = 0; i < W::IPK; ++i)
-      dma16_buf(krsrc[i], kvoff[i], (QA_DQW_DIAG & 2) ? 0u : (unsigned)min(t, nt - 1) * 64u * D, sl + klds[i]);
+      if (!(QA_DQW_DIAG & 8)) dma16_buf(krsrc[i], kvoff[i], (QA_DQW_DIAG & 2) ? 0u : (unsigned)min(t, nt - 1) * 64u * D, sl + klds[i]);
   };
   auto issue_r = [&](int t, int rs) {   // record of tile t into ring slot rs; read once: non-temporal
+    if (QA_DQW_DIAG & 4) return;
 #if QA_DQW_NT
     dma16_buf_nt(rrsrc, 16u * lane, (QA_DQW_DIAG & 1) ? 0u : (unsigned)min(t, nt - 1) * 1024u,
 #else
