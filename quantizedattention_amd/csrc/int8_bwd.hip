@@ -1103,214 +1103,6 @@ __global__ __launch_bounds__(64 * QA_DQW_WAVES, QA_DQW_WAVES >= 16 ? 4 : 2) void
   }
 }
 
-// ------------------------------------------------ dQ from the dS workspace, role-split (A/B)
-// The same products as int8_bwd_dqw_kernel, split by role (MI355X_MICROARCH / DESIGN.md §5: a wave
-// that mixes MFMAs and vector work costs the SUM of their issue time, a vector-only wave beside an
-// MFMA-only wave overlaps with it): CW consumer waves own 32 queries each and only read the k image
-// and their operands from LDS and issue the 8 bf16 MFMAs per tile; PW producer waves issue every
-// LDS-DMA (k image and records) and form the consumers' bf16 operands (the record read, the
-// permutation MFMA, the conversions, exactly make_op), handing them over through an operand ring in
-// LDS.  One workgroup barrier per tile.  Consumers load tile t+1's k image and operands before the
-// MFMAs of tile t (registers, so the MFMAs start at the barrier), producers form tile t+2's operands
-// in iteration t (three operand slots).  dq bit-identical.
-#ifndef QA_DQW_RS
-#define QA_DQW_RS 0
-#endif
-#ifndef QA_DQW_RS_PW
-#define QA_DQW_RS_PW 4
-#endif
-#ifndef QA_DQW_RS_NSLOT
-#define QA_DQW_RS_NSLOT 5
-#endif
-#ifndef QA_DQW_RS_RSLOT
-#define QA_DQW_RS_RSLOT 6
-#endif
-template <int D>
-struct DqwRsCfg {
-  static constexpr int CW = 8, PW = QA_DQW_RS_PW, WAVES = CW + PW;
-  static_assert(CW % PW == 0, "every producer serves the same number of consumers");
-  static constexpr int RPP = CW / PW;              // consumers (records) per producer
-  static constexpr int T16 = 64 * D;
-  static constexpr int NSLOT = QA_DQW_RS_NSLOT, RSLOT = QA_DQW_RS_RSLOT;
-  static_assert(NSLOT >= 4, "k image ring: tiles t, t+1 in use, t+2.. landing");
-  static_assert(RSLOT >= NSLOT + 1, "records run one tile further ahead than the k image");
-  static constexpr int REC = CW * 1024;            // the consumers' records of one tile
-  static constexpr int OPB = CW * 2048;            // their bf16 operands of one tile
-  static constexpr int OSLOT = 3;
-  static constexpr int NP16 = T16 / 1024;
-  static constexpr int KPP = (NP16 + PW - 1) / PW; // k image pieces per producer per tile
-  static constexpr int RBASE = NSLOT * T16, OBASE = RBASE + RSLOT * REC, CBASE = OBASE + OSLOT * OPB;
-  // At the top of iteration t the barrier needs k(t+1) (issued in iteration t-NSLOT+2) and the
-  // records of t+2 (iteration t-RSLOT+3, at or before it): the producer DMAs younger than k(t+1)
-  static constexpr int WAITN = (RSLOT - 1 > NSLOT ? RPP : 0) + (NSLOT - 3) * (KPP + RPP);
-};
-
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(64 * DqwRsCfg<D>::WAVES, 1) void int8_bwd_dqw_rs_kernel(
-    const int8_t* __restrict__ ds8, const float* __restrict__ sds, const __bf16* __restrict__ kbf,
-    const _Float16* __restrict__ sk, _Float16* __restrict__ dq, int BH, int Sq, int Sk, int G,
-    float sms) {
-  using C = I8BwdCfg<D>;
-  using W = DqwRsCfg<D>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nqb = (Sq + 32 * W::CW - 1) / (32 * W::CW);
-  int bh, qb;
-  if constexpr (CAUSAL && QA_DQW_HG > 0) xcd_remap_lpt_grouped(blockIdx.x, nqb, BH, true, QA_DQW_HG, bh, qb);
-  else if constexpr (CAUSAL) xcd_remap_lpt(blockIdx.x, nqb, BH, true, bh, qb);
-  else xcd_remap(blockIdx.x, nqb, BH, bh, qb);
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const bool producer = wave >= W::CW;
-  const int nqt = Sq / 32, nkt = Sk / 32;
-  const long kv_row0 = (long)(bh / G) * Sk;
-  const int nt = CAUSAL ? min(nkt, (qb * 32 * W::CW + 32 * W::CW) / 32) : nkt;
-  const int qw0 = qb * 32 * W::CW;                 // the workgroup's first query
-  const unsigned smem_lds = lds_addr(smem);
-  float* c_lds = reinterpret_cast<float*>(smem + W::CBASE);
-
-  if (producer) {
-    // ---------------------------------------------------------------- producer
-    const int p = wave - W::CW;
-    unsigned kvoff[W::KPP], klds[W::KPP];
-#pragma unroll
-    for (int i = 0; i < W::KPP; ++i) {
-      int pc = p + W::PW * i;
-      if (pc >= W::NP16) pc = p % W::NP16;   // padding piece: the same bytes to the same place
-      constexpr int NCH = 2 * D / 16, RPI = 64 / NCH;
-      const int row = pc * RPI + lane / NCH, c = lane % NCH;
-      kvoff[i] = row * 2 * D + 16 * (c ^ t16_sw<D>(row));
-      klds[i] = pc * 1024;
-    }
-    const v4u krsrc = make_rsrc(kbf + kv_row0 * D, (unsigned)Sk * 2 * D);
-    v4u rrsrc[W::RPP];
-#pragma unroll
-    for (int j = 0; j < W::RPP; ++j) {
-      const int w = p * W::RPP + j, q0 = qw0 + 32 * w;
-      const bool act = q0 < Sq;
-      const long rec0 = ((long)bh * nqt + (act ? q0 / 32 : 0)) * nkt;
-      rrsrc[j] = make_rsrc(ds8 + rec0 * 1024, act ? (unsigned)nkt * 1024u : 0u);
-    }
-    auto issue_k = [&](int tk) {
-      const unsigned sl = smem_lds + (tk % W::NSLOT) * W::T16;
-#pragma unroll
-      for (int i = 0; i < W::KPP; ++i) dma16_buf(krsrc, kvoff[i], (unsigned)min(tk, nt - 1) * 64u * D, sl + klds[i]);
-    };
-    auto issue_r = [&](int tr) {
-#pragma unroll
-      for (int j = 0; j < W::RPP; ++j)
-        dma16_buf_nt(rrsrc[j], 16u * lane, (unsigned)min(tr, nt - 1) * 1024u,
-                     smem_lds + W::RBASE + (tr % W::RSLOT) * W::REC + (p * W::RPP + j) * 1024);
-    };
-    // permutation operand (as int8_bwd_dqw_kernel)
-    v4i perm = {0, 0, 0, 0};
-    if (((c32 >> 2) & 1) == h) {
-      const int i = 4 * (c32 >> 3) + (c32 & 3);
-      perm[i >> 2] = 1 << (8 * (i & 3));
-    }
-    // the operands of tile t for this producer's consumers, into operand slot t % OSLOT
-    auto produce = [&](int t) {
-#pragma unroll
-      for (int j = 0; j < W::RPP; ++j) {
-        const int w = p * W::RPP + j;
-        const float c = c_lds[w * nkt + t];
-        const v4i rec = *reinterpret_cast<const v4i*>(smem + W::RBASE + (t % W::RSLOT) * W::REC +
-                                                      w * 1024 + 16 * (lane ^ ((lane >> 5) << 2)));
-        const v16i x = mfma_i8(rec, perm, v16i{});
-        char* ob = smem + W::OBASE + (t % W::OSLOT) * W::OPB + w * 2048 + 16 * lane;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          v4u wd;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) wd[k] = pk_bf16((float)x[8 * s + 2 * k] * c, (float)x[8 * s + 2 * k + 1] * c);
-          *reinterpret_cast<v4u*>(ob + 1024 * s) = wd;
-        }
-      }
-    };
-    for (int i = 0; i < W::NSLOT - 1; ++i) issue_k(i);
-    for (int i = 0; i < W::RSLOT - 1; ++i) issue_r(i);
-    vmem_drain();
-    __syncthreads();   // (1) records 0 .. RSLOT-2 landed, the consumers' scales written
-    produce(0);
-    if (nt > 1) produce(1);
-    __syncthreads();   // (2) operands of tiles 0 and 1 written
-    for (int t = 0; t < nt; ++t) {
-      ring_wait_barrier<W::WAITN>();
-      // slots written here: k image (t-1) % NSLOT, records (t-1) % RSLOT, operands (t+2) % 3 --
-      // none of them read in this iteration or later by what is in flight
-      issue_k(t + W::NSLOT - 1);
-      issue_r(t + W::RSLOT - 1);
-      if (t + 2 < nt) produce(t + 2);
-    }
-    vmcnt_wait_all();
-    return;
-  }
-
-  // ---------------------------------------------------------------- consumer
-  const int q0 = qw0 + wave * 32;
-  const bool active = q0 < Sq;
-  {
-    const long rec0 = ((long)bh * nqt + (active ? q0 / 32 : 0)) * nkt;
-    for (int i = lane; i < nt; i += 64) c_lds[wave * nkt + i] = active ? sds[rec0 + i] * (float)sk[kv_row0 / 32 + i] : 0.f;
-  }
-  int troff[C::NDB];
-  {
-    const int gg = (lane >> 4) & 1, i16 = lane & 15;
-    const int row = 4 * h + (i16 >> 2);
-#pragma unroll
-    for (int b = 0; b < C::NDB; ++b) {
-      const int d = 32 * b + 16 * gg + 4 * (i16 & 3);
-      troff[b] = row * 2 * D + 16 * ((d / 8) ^ t16_sw<D>(row)) + (d % 8) * 2;
-    }
-  }
-  v16f acc[C::NDB];
-#pragma unroll
-  for (int b = 0; b < C::NDB; ++b) acc[b] = v16f{};
-  // tile t's operands (k image fragments and the bf16 dS operand) into registers
-  auto load = [&](int t, v8bf* ta, v8bf* op) {
-    const char* kb = smem + (t % W::NSLOT) * W::T16;
-    const char* ob = smem + W::OBASE + (t % W::OSLOT) * W::OPB + wave * 2048 + 16 * lane;
-    op[0] = *reinterpret_cast<const v8bf*>(ob);
-    op[1] = *reinterpret_cast<const v8bf*>(ob + 1024);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int b = 0; b < C::NDB; ++b) {
-        const char* a = kb + troff[b] + 16 * s * 2 * D;
-        ta[s * C::NDB + b] = __builtin_bit_cast(v8bf, ds_read_tr16_x2(a, a + 8 * 2 * D));
-      }
-  };
-  __syncthreads();   // (1)
-  __syncthreads();   // (2)
-  v8bf ta[2 * C::NDB], op[2];
-  load(0, ta, op);
-  for (int t = 0; t < nt; ++t) {
-    ring_wait_barrier<0>();
-    v8bf tn[2 * C::NDB], on[2];
-    load(min(t + 1, nt - 1), tn, on);   // (the last iteration re-loads tile nt-1: discarded)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int b = 0; b < C::NDB; ++b) acc[b] = mfma_bf16(ta[s * C::NDB + b], op[s], acc[b]);
-#pragma unroll
-    for (int i = 0; i < 2 * C::NDB; ++i) ta[i] = tn[i];
-    op[0] = on[0];
-    op[1] = on[1];
-  }
-  if (!active) return;
-  const long r = (long)bh * Sq + q0 + c32;
-#pragma unroll
-  for (int b = 0; b < C::NDB; ++b) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      v4h w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = (_Float16)(acc[b][4 * g + j] * sms);
-      *reinterpret_cast<v4h*>(dq + r * D + 32 * b + 8 * g + 4 * h) = w;
-    }
-  }
-}
-
 }  // namespace qattn
 
 using namespace qattn;
@@ -1383,16 +1175,6 @@ template <int D, bool CAUSAL>
 static void launch_dqw_c(const void* ds8, const void* sds, const void* k_bf, const void* sk, void* dq,
                          long bh, long sqt, long skt, int group, float sms, hipStream_t st) {
   const int nkt = (int)(skt / 32);
-  if constexpr (QA_DQW_RS) {
-    using R = DqwRsCfg<D>;
-    const int lds = R::CBASE + R::CW * nkt * 4 + 16;
-    { static int granted_ = 0; lds_grant((const void*)int8_bwd_dqw_rs_kernel<D, CAUSAL>, lds, granted_); }
-    const int nb = (int)((sqt + 32 * R::CW - 1) / (32 * R::CW));
-    hipLaunchKernelGGL((int8_bwd_dqw_rs_kernel<D, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * R::WAVES),
-                       lds, st, (const int8_t*)ds8, (const float*)sds, (const __bf16*)k_bf,
-                       (const _Float16*)sk, (_Float16*)dq, (int)bh, (int)sqt, (int)skt, group, sms);
-    return;
-  }
   using G = DqwCfg<D>;
   const int lds = G::RBASE + G::RSLOT * G::REC + G::WAVES * nkt * 4 + 16;
   { static int granted_ = 0; lds_grant((const void*)int8_bwd_dqw_kernel<D, CAUSAL>, lds, granted_); }
