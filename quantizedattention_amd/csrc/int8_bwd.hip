@@ -1174,8 +1174,8 @@ static void launch_bwd(int causal, const void* x8a, const void* x8b, const void*
 template <int D, bool CAUSAL>
 static void launch_dqw_c(const void* ds8, const void* sds, const void* k_bf, const void* sk, void* dq,
                          long bh, long sqt, long skt, int group, float sms, hipStream_t st) {
-  const int nkt = (int)(skt / 32);
   using G = DqwCfg<D>;
+  const int nkt = (int)(skt / 32);
   const int lds = G::RBASE + G::RSLOT * G::REC + G::WAVES * nkt * 4 + 16;
   { static int granted_ = 0; lds_grant((const void*)int8_bwd_dqw_kernel<D, CAUSAL>, lds, granted_); }
   const int nb = (int)((sqt + 32 * G::WAVES - 1) / (32 * G::WAVES));
