@@ -29,5 +29,5 @@ for _ in range(7):
 h = hashlib.sha256()
 for x in out[:3]:
     h.update(x.contiguous().view(torch.int16).cpu().numpy().tobytes())
-print(f"chunk={os.environ.get('QATTN_BWD_WS_CHUNK', 'auto')} dkv_chunk={os.environ.get('QATTN_BWD_WS_DKV_CHUNK', 'auto')}: causal backward {sorted(ts)[3]:.3f} ms, "
+print(f"chunk={os.environ.get('QATTN_BWD_WS_CHUNK', 'auto')}: causal backward {sorted(ts)[3]:.3f} ms, "
       f"grads {h.hexdigest()[:12]}", flush=True)
