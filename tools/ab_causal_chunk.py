@@ -1,5 +1,6 @@
 """Causal int8 backward at config 3 by chunk size (dev tool): QATTN_BWD_WS_CHUNK=<kv heads per chunk>
-python tools/ab_causal_chunk.py  -> median ms of _int8_backward(causal=True) and an output digest."""
+python tools/ab_causal_chunk.py  -> median ms of _int8_backward(causal=True) and an output digest
+(AB_CAUSAL=0: the non-causal backward)."""
 import hashlib
 import os
 import sys
@@ -11,10 +12,11 @@ from quantizedattention_amd.attention_int8 import _int8_backward, _int8_forward 
 
 g = torch.Generator(device="cuda").manual_seed(0)
 B, H, S, D = 4, 32, 4096, 128
+causal = os.environ.get("AB_CAUSAL", "1") == "1"
 q, k, v = (torch.randn((B, H, S, D), device="cuda", generator=g).half() for _ in range(3))
 dO = (torch.randn((B, H, S, D), device="cuda", generator=g) * 1e-3).half()
-O, lse, qi, kiT, vi, sq, sk, sv, km, qb, kb = _int8_forward(q, k, v, smooth=True, images=True, causal=True)
-f = lambda: _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb, kb, causal=True)  # noqa: E731
+O, lse, qi, kiT, vi, sq, sk, sv, km, qb, kb = _int8_forward(q, k, v, smooth=True, images=True, causal=causal)
+f = lambda: _int8_backward(dO, qi, sq, kiT, sk, vi, sv, O, lse, qb, kb, causal=causal)  # noqa: E731
 for _ in range(2):
     out = f()
 torch.cuda.synchronize()
@@ -29,5 +31,5 @@ for _ in range(7):
 h = hashlib.sha256()
 for x in out[:3]:
     h.update(x.contiguous().view(torch.int16).cpu().numpy().tobytes())
-print(f"chunk={os.environ.get('QATTN_BWD_WS_CHUNK', 'auto')}: causal backward {sorted(ts)[3]:.3f} ms, "
+print(f"chunk={os.environ.get('QATTN_BWD_WS_CHUNK', 'auto')}: {'causal' if causal else 'non-causal'} backward {sorted(ts)[3]:.3f} ms, "
       f"grads {h.hexdigest()[:12]}", flush=True)
