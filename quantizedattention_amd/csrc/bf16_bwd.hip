@@ -782,7 +782,7 @@ static void launch_b16c(const void* xa, const void* xb, const void* ya, const vo
     if constexpr (ROLE == B16_DKV) return bf16_bwd_dkv_kernel<D, CAUSAL, WS>;
     else return bf16_bwd_kernel<D, ROLE, CAUSAL>;
   }();
-  { static int granted_ = 0; lds_grant((const void*)kern, G::LDS, granted_); }
+  { static LdsGrant granted_; lds_grant((const void*)kern, G::LDS, granted_); }
   const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
   hipLaunchKernelGGL(kern, dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
                      G::LDS, st, (const _Float16*)xa, (const __bf16*)xb, (const _Float16*)ya,
@@ -808,7 +808,7 @@ template <int D, bool CAUSAL>
 static void launch_dqw_b16c(const void* ws, const void* k_bf, void* dq, long bh, long sq, long sk,
                             int group, float sms, hipStream_t st) {
   using W = B16DqwCfg<D>;
-  { static int granted_ = 0; lds_grant((const void*)bf16_bwd_dqw_kernel<D, CAUSAL>, W::LDS, granted_); }
+  { static LdsGrant granted_; lds_grant((const void*)bf16_bwd_dqw_kernel<D, CAUSAL>, W::LDS, granted_); }
   const int nb = (int)((sq + 32 * W::WAVES - 1) / (32 * W::WAVES));
   hipLaunchKernelGGL((bf16_bwd_dqw_kernel<D, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * W::WAVES),
                      W::LDS, st, (const __bf16*)ws, (const __bf16*)k_bf, (float*)dq, (int)bh, (int)sq,

@@ -476,7 +476,7 @@ extern "C" int qattn_bf16_fwd_ws_ex(const void* q, const void* k, const void* v,
   {                                                                                              \
     using C = Bf16FwdCfg<Dv>;                                                                    \
     const int nq = (int)((sq + C::QROWS - 1) / C::QROWS);                                        \
-    { static int granted_ = 0; lds_grant((const void*)bf16_fwd_kernel<Dv, CV, SV>, C::LDS, granted_); } \
+    { static LdsGrant granted_; lds_grant((const void*)bf16_fwd_kernel<Dv, CV, SV>, C::LDS, granted_); } \
     hipLaunchKernelGGL((bf16_fwd_kernel<Dv, CV, SV>), dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), \
                        C::LDS, st, (const _Float16*)q, (const _Float16*)k, (const __bf16*)v,     \
                        (float*)out, (float*)lse, (int)bh, (int)sq, (int)sk, group, qks,          \

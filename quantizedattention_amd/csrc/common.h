@@ -39,7 +39,20 @@ typedef int v2i __attribute__((ext_vector_type(2)));
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) only when a launch needs more dynamic LDS than
 // the kernel was granted so far: `granted` is a static of the calling launch function (one per
 // kernel instantiation), so steady-state launches (decode steps of ~50 us) make no attribute call.
-inline bool lds_grant(const void* kernel, int bytes, int& granted) {
+// The attribute belongs to the kernel on the CURRENT device, so the grant is kept per device (one
+// process driving several GPUs must set it on each).
+struct LdsGrant {
+  static constexpr int MAX_DEV = 64;
+  int bytes[MAX_DEV] = {};
+};
+inline bool lds_grant(const void* kernel, int bytes, LdsGrant& grants) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= LdsGrant::MAX_DEV) {
+    (void)hipGetLastError();
+    dev = -1;   // (unknown device: set the attribute, remember nothing)
+  }
+  int scratch = 0;
+  int& granted = dev >= 0 ? grants.bytes[dev] : scratch;
   if (bytes <= granted) return true;
   if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
     // clear the runtime's last error: the caller reports the refusal (status 1), and a stale

@@ -779,7 +779,7 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
   constexpr bool INL = QA_FWD_INLINE_FIX && QF && C::LIT_K > 0 && QA_FWD_DEFER;
   auto kern = int8_attn_fwd_kernel<D, CAUSAL, false, QF, false, INL>;
   const int lds_k = lds + (INL ? 4 * C::WAVES : 0);
-  { static int granted_ = 0; if (!lds_grant((const void*)kern, lds_k, granted_)) return 1; }
+  { static LdsGrant granted_; if (!lds_grant((const void*)kern, lds_k, granted_)) return 1; }
   hipLaunchKernelGGL(kern, dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds_k, st,
                      (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
                      (const int8_t*)vt, (const _Float16*)sv, (_Float16*)out, (_Float16*)lse, (int)bh,
@@ -787,7 +787,7 @@ static int launch_fwd(const void* q_i8, const void* sq, const void* k_i8, const 
   if constexpr (C::LIT_K > 0 && QA_FWD_DEFER && !INL) {   // the waves whose votes held: redone
     if (skip_fixup()) return hipGetLastError() == hipSuccess ? 0 : 2;
     auto fixk = int8_attn_fwd_kernel<D, CAUSAL, false, false, true>;
-    { static int granted_ = 0; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
+    { static LdsGrant granted_; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
     hipLaunchKernelGGL(fixk, dim3((unsigned)(nq * bh)), dim3(64 * C::WAVES), lds, st,
                        (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
                        (const int8_t*)vt, (const _Float16*)sv, (_Float16*)out, (_Float16*)lse, (int)bh,
@@ -837,7 +837,7 @@ static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, 
   const int nq = (int)((sq_tok + C::QROWS - 1) / C::QROWS);
   const int nsplit = (int)((sk_tok + ks - 1) / ks);
   const int lds = C::lds_bytes(ks / 32);
-  { static int granted_ = 0; if (!lds_grant((const void*)int8_attn_fwd_kernel<D, false, true>, lds, granted_)) return 1; }
+  { static LdsGrant granted_; if (!lds_grant((const void*)int8_attn_fwd_kernel<D, false, true>, lds, granted_)) return 1; }
   hipLaunchKernelGGL((int8_attn_fwd_kernel<D, false, true>), dim3((unsigned)(nq * bh), (unsigned)nsplit),
                      dim3(64 * C::WAVES), lds, st, (const int8_t*)q_i8, (const _Float16*)sq,
                      (const int8_t*)k_i8, (const _Float16*)sk, (const int8_t*)vt, (const _Float16*)sv,
@@ -846,7 +846,7 @@ static int launch_fwd_split(const void* q_i8, const void* sq, const void* k_i8, 
   if constexpr (C::LIT_K > 0 && QA_FWD_DEFER) {   // the split rows whose first tile must be redone
     if (skip_fixup()) return hipGetLastError() == hipSuccess ? 0 : 2;
     auto fixk = int8_attn_fwd_kernel<D, false, true, false, true>;
-    { static int granted_ = 0; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
+    { static LdsGrant granted_; if (!lds_grant((const void*)fixk, lds, granted_)) return 1; }
     hipLaunchKernelGGL(fixk, dim3((unsigned)(nq * bh), (unsigned)nsplit), dim3(64 * C::WAVES), lds, st,
                        (const int8_t*)q_i8, (const _Float16*)sq, (const int8_t*)k_i8, (const _Float16*)sk,
                        (const int8_t*)vt, (const _Float16*)sv, (_Float16*)opart, (_Float16*)ml, (int)bh,

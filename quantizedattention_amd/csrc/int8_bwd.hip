@@ -1147,7 +1147,7 @@ static void launch_bwd_c(const void* x8a, const void* x8b, const void* sxa, cons
   using G = BwdCfg<D, ROLE>;
   const int lds = G::NSLOT * G::SLOT + (int)((2 * (ny / 32) * 2 + 15) / 16 * 16) +
                   (WS ? G::WAVES * (int)(ny / 32) * 4 : 0);
-  { static int granted_ = 0; lds_grant((const void*)int8_bwd_kernel<D, ROLE, CAUSAL, WS>, lds, granted_); }
+  { static LdsGrant granted_; lds_grant((const void*)int8_bwd_kernel<D, ROLE, CAUSAL, WS>, lds, granted_); }
   const int nb = (int)((sx + G::XROWS - 1) / G::XROWS);
   hipLaunchKernelGGL((int8_bwd_kernel<D, ROLE, CAUSAL, WS>), dim3((unsigned)(nb * bhx)),
                      dim3(64 * G::WAVES), lds, st, (const int8_t*)x8a, (const int8_t*)x8b,
@@ -1177,7 +1177,7 @@ static void launch_dqw_c(const void* ds8, const void* sds, const void* k_bf, con
   using G = DqwCfg<D>;
   const int nkt = (int)(skt / 32);
   const int lds = G::RBASE + G::RSLOT * G::REC + G::WAVES * nkt * 4 + 16;
-  { static int granted_ = 0; lds_grant((const void*)int8_bwd_dqw_kernel<D, CAUSAL>, lds, granted_); }
+  { static LdsGrant granted_; lds_grant((const void*)int8_bwd_dqw_kernel<D, CAUSAL>, lds, granted_); }
   const int nb = (int)((sqt + 32 * G::WAVES - 1) / (32 * G::WAVES));
   hipLaunchKernelGGL((int8_bwd_dqw_kernel<D, CAUSAL>), dim3((unsigned)(nb * bh)), dim3(64 * G::WAVES),
                      lds, st, (const int8_t*)ds8, (const float*)sds, (const __bf16*)k_bf,

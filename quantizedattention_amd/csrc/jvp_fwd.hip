@@ -311,7 +311,7 @@ using namespace qattn;
 template <int D, bool X3, bool TAN = true>
 static int launch_jvp(const JvpArgs& a, long bh, long sq, hipStream_t st) {
   constexpr int lds = 2 * JvpCfg<D, X3, TAN>::STAGE;
-  { static int granted_ = 0; lds_grant((const void*)jvp_fwd_kernel<D, X3, TAN>, lds, granted_); }
+  { static LdsGrant granted_; lds_grant((const void*)jvp_fwd_kernel<D, X3, TAN>, lds, granted_); }
   const int nq = (int)((sq + 127) / 128);
   hipLaunchKernelGGL((jvp_fwd_kernel<D, X3, TAN>), dim3((unsigned)(nq * bh)), dim3(256), lds, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;

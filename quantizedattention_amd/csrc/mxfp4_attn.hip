@@ -328,7 +328,7 @@ extern "C" int qattn_mxfp4_attn_fwd(const void* q4, const void* qscale, const vo
   using C = MxCfg<128>;
   const int nq = (int)((sq + C::QROWS - 1) / C::QROWS);
   const int lds = C::NSLOT * C::SLOT;
-  { static int granted_ = 0; lds_grant((const void*)mxfp4_attn_fwd_kernel<128>, lds, granted_); }
+  { static LdsGrant granted_; lds_grant((const void*)mxfp4_attn_fwd_kernel<128>, lds, granted_); }
   hipLaunchKernelGGL((mxfp4_attn_fwd_kernel<128>), dim3((unsigned)(nq * bh)), dim3(256), lds,
                      (hipStream_t)stream, (const uint8_t*)q4, (const uint8_t*)qscale, (const uint8_t*)k4,
                      (const uint8_t*)kscale, (const uint8_t*)vt, (const uint8_t*)vscale, (_Float16*)out,
